@@ -1,0 +1,237 @@
+/*
+ * npr.h — C-ABI of the MI355X-native pcap record parser + flow extractor.
+ *
+ * This is the drop-in boundary for the hot path of protectwise/net-parser-rs 0.3.0:
+ * the nom parse paths of src/global_header.rs, src/record.rs, src/file.rs, src/layer2,
+ * src/layer3, src/layer4 and src/flow.  The reference has no FFI of its own (it is a pure
+ * Rust crate); every entry point below names the reference function it replaces, and
+ * INTEGRATION.md shows the `extern "C"` block a Rust maintainer would add to bind it.
+ *
+ * Conventions
+ *   - Plain pointers and sizes only; no torch / HIP types in any signature
+ *     (streams are passed as `void*` = hipStream_t, NULL = the context's own stream).
+ *   - Results carry BYTE OFFSETS into the caller's buffer, never pointers: the Rust API
+ *     borrows the input slice (`&'a [u8]`), an offset is the FFI-safe equivalent.
+ *   - Status codes 1..3 map 1:1 onto crate::errors::Error (src/errors.rs:3-11);
+ *     negative codes are boundary errors the Rust API cannot produce.
+ *   - A context is per host thread (the Rust functions are pure and reentrant; a context
+ *     owns one device, one stream and its workspaces, so give each thread its own).
+ */
+#ifndef NPR_H
+#define NPR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NPR_ABI_VERSION 1
+
+/* ---- status of an API call ------------------------------------------------------------ */
+typedef enum npr_status {
+  NPR_OK = 0,
+  NPR_INCOMPLETE = 1,      /* crate::errors::Error::Incomplete  (src/errors.rs:5)  */
+  NPR_FAILURE = 2,         /* crate::errors::Error::Failure     (src/errors.rs:7)  */
+  NPR_CUSTOM = 3,          /* crate::errors::Error::Custom      (src/errors.rs:9)  */
+  NPR_ERR_ARG = -1,        /* bad argument (null pointer, misaligned device buffer, ...) */
+  NPR_ERR_DEVICE = -2,     /* HIP runtime error; see npr_ctx_last_error() */
+  NPR_ERR_CAPACITY = -3,   /* an output array was too small; counts are still exact */
+  NPR_ERR_TIMEOUT = -4,    /* tile hand-off did not complete (guard against a stalled grid) */
+  NPR_ERR_NOMEM = -5
+} npr_status;
+
+/* nom::Endianness as chosen by GlobalHeader::parse (src/global_header.rs:43-53) */
+typedef enum npr_endianness { NPR_LITTLE = 0, NPR_BIG = 1 } npr_endianness;
+
+/* GlobalHeader (src/global_header.rs:13-23) */
+typedef struct npr_global_header {
+  int32_t endianness; /* npr_endianness */
+  uint16_t version_major;
+  uint16_t version_minor;
+  int32_t zone;
+  int32_t sig_figs;
+  uint32_t snap_length;
+  uint32_t network;
+} npr_global_header;
+
+/* PcapRecord (src/record.rs:59-65).  `payload` = input[offset+16 .. offset+16+actual_length];
+ * timestamp = UNIX_EPOCH + ts_sec s + ts_usec us (convert_packet_time, src/record.rs:82-86). */
+typedef struct npr_record {
+  uint64_t offset;          /* byte offset of the 16-B record header in the input */
+  uint32_t ts_sec;
+  uint32_t ts_usec;
+  uint32_t actual_length;   /* incl_len */
+  uint32_t original_length; /* orig_len */
+} npr_record;
+
+/* Flow (src/flow/mod.rs:53-61) in a fixed 32-byte encoding.
+ *   layer2 is always Ethernet (the only info::layer2::Id, src/flow/info.rs:8-10).
+ *   kind bit0: layer3  0 = IPv4, 1 = IPv6      (info::layer3::Id; Arp never yields a flow)
+ *   kind bit1: layer4  0 = Tcp,  1 = Udp       (info::layer4::Id; Vxlan is never produced)
+ *   src_ip/dst_ip: the 4 address bytes in packet order for IPv4; 0 for IPv6, whose 16-byte
+ *   addresses live in npr_flow_v6 at the same index.
+ *   record_offset: 40-bit little-endian byte offset of the flow's record header (the
+ *   `PcapRecord` half of convert_records' `(PcapRecord, Flow)` pair). */
+typedef struct npr_flow {
+  uint8_t src_ip[4];
+  uint8_t dst_ip[4];
+  uint16_t src_port;
+  uint16_t dst_port;
+  uint16_t vlan;
+  uint8_t src_mac[6];
+  uint8_t dst_mac[6];
+  uint8_t kind;
+  uint8_t record_offset[5];
+} npr_flow;
+
+typedef struct npr_flow_v6 {
+  uint8_t src_ip[16];
+  uint8_t dst_ip[16];
+} npr_flow_v6;
+
+#define NPR_FLOW_KIND_IPV6 0x1u
+#define NPR_FLOW_KIND_UDP 0x2u
+
+/* Per-record result of extract_flow: one code per leaf of the reference's error tree
+ * flow::errors::Error (src/flow/errors.rs:5-19) and its per-layer `errors` modules. */
+typedef enum npr_flow_status {
+  NPR_FLOW_OK = 0,
+  /* Error::NetParser(e): Ethernet::parse failed (src/flow/mod.rs:28-31) */
+  NPR_FLOW_ETH_INCOMPLETE = 1, /* e = Incomplete: < 14 B, or a truncated 802.1Q/ad tag  */
+  NPR_FLOW_ETH_FAILURE = 2,    /* e = Failure: unknown EtherType (src/layer2/ethernet.rs:57-73) */
+  /* Error::L2(Ethernet(EthernetType{..})): LLDP or an 802.3 length (src/flow/layer2/ethernet.rs:125-130) */
+  NPR_FLOW_L2_ETHERTYPE = 3,
+  /* Error::L2(Ethernet(NetParser{l3, err})) */
+  NPR_FLOW_L2_IPV4_INCOMPLETE = 4,
+  NPR_FLOW_L2_IPV4_FAILURE = 5, /* unknown protocol id (src/layer3/mod.rs:54-72) */
+  NPR_FLOW_L2_IPV4_CUSTOM = 6,  /* version != 4 (src/layer3/ipv4.rs:156) */
+  NPR_FLOW_L2_IPV6_INCOMPLETE = 7,
+  NPR_FLOW_L2_IPV6_FAILURE = 8,
+  NPR_FLOW_L2_IPV6_CUSTOM = 9,
+  NPR_FLOW_L2_ARP_INCOMPLETE = 10,
+  /* Error::L2(Ethernet(Incomplete{l3, size})): bytes left after the L3 parse */
+  NPR_FLOW_L2_IPV4_REMAINDER = 11,
+  NPR_FLOW_L2_IPV6_REMAINDER = 12,
+  NPR_FLOW_L2_ARP_REMAINDER = 13,
+  /* Error::L3(Arp(Flow)) (src/flow/layer3/arp.rs:23-27) */
+  NPR_FLOW_L3_ARP = 14,
+  /* Error::L3(IPv4|IPv6(InternetProtocolId{id})): neither TCP nor UDP */
+  NPR_FLOW_L3_IPV4_PROTOCOL = 15,
+  NPR_FLOW_L3_IPV6_PROTOCOL = 16,
+  /* Error::L3(IPv4|IPv6(NetParser{l4, err})) */
+  NPR_FLOW_L3_IPV4_TCP_INCOMPLETE = 17,
+  NPR_FLOW_L3_IPV4_TCP_FAILURE = 18, /* data offset outside [20, 60] (src/layer4/tcp.rs:68-82) */
+  NPR_FLOW_L3_IPV4_UDP_INCOMPLETE = 19,
+  NPR_FLOW_L3_IPV6_TCP_INCOMPLETE = 20,
+  NPR_FLOW_L3_IPV6_TCP_FAILURE = 21,
+  NPR_FLOW_L3_IPV6_UDP_INCOMPLETE = 22,
+  /* Error::L3(IPv4|IPv6(Incomplete{l4: Udp, size})): UDP length != L3 payload length */
+  NPR_FLOW_L3_IPV4_UDP_REMAINDER = 23,
+  NPR_FLOW_L3_IPV6_UDP_REMAINDER = 24,
+  NPR_FLOW_STATUS_COUNT = 25
+} npr_flow_status;
+
+/* Totals written by the device at the end of a parse.  `consumed` is where the record
+ * chain stopped: the Rust remainder slice is input[consumed..] (src/record.rs:51). */
+typedef struct npr_summary {
+  uint64_t n_records;
+  uint64_t n_flows;
+  uint64_t consumed;
+  uint32_t flags; /* NPR_SUMMARY_* */
+  uint32_t epoch;
+} npr_summary;
+
+#define NPR_SUMMARY_RECORD_OVERFLOW 0x1u /* record_cap too small */
+#define NPR_SUMMARY_FLOW_OVERFLOW 0x2u   /* flow_cap too small */
+
+/* Device-resident outputs of npr_dev_parse_extract.  Any array may be NULL (not produced).
+ *   record_offsets/records/record_status: dense, file order (PcapRecords::parse order);
+ *   `records` is the full PcapRecord row, `record_offsets` just its offset.
+ *   flows/flows_v6: convert_records order (reverse file order, Ok flows only,
+ *   src/flow/mod.rs:101-123), RIGHT-ALIGNED: the valid range is
+ *   [flow_cap - n_flows, flow_cap).  flows_v6[i] is written only when flows[i] is IPv6.
+ *   summary: device pointer, always written. */
+typedef struct npr_dev_outputs {
+  uint64_t *record_offsets;
+  npr_record *records;
+  uint8_t *record_status;
+  uint64_t record_cap;
+  npr_flow *flows;
+  npr_flow_v6 *flows_v6;
+  uint64_t flow_cap;
+  npr_summary *summary;
+} npr_dev_outputs;
+
+/* ---- library / context ---------------------------------------------------------------- */
+typedef struct npr_ctx npr_ctx;
+
+const char *npr_version(void);
+int npr_abi_version(void);
+/* Create a context on HIP device `device` (one stream, workspaces grown on demand). */
+npr_status npr_ctx_create(int device, npr_ctx **out);
+void npr_ctx_destroy(npr_ctx *ctx);
+const char *npr_ctx_last_error(const npr_ctx *ctx);
+/* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
+uint64_t npr_workspace_bytes(uint64_t len);
+
+/* ---- host-side, single objects (no device work: 24 B / 16 B) ----------------------------- */
+/* GlobalHeader::parse (src/global_header.rs:40-70). *consumed = 24 on success. */
+npr_status npr_global_header_parse(const uint8_t *input, size_t len, npr_global_header *out,
+                                   size_t *consumed);
+/* PcapRecord::parse (src/record.rs:102-121). *consumed = 16 + actual_length. */
+npr_status npr_record_parse(const uint8_t *input, size_t len, npr_endianness endianness,
+                            npr_record *out, size_t *consumed);
+
+/* ---- host-memory entry points (stage to HBM, run the device path, copy back) ------------- */
+/* PcapRecords::parse (src/record.rs:21-54): records from byte 0, stop at the first Incomplete.
+ * Writes up to `cap` records; *n_out = total found (> cap => NPR_ERR_CAPACITY). */
+npr_status npr_records_parse(npr_ctx *ctx, const uint8_t *input, size_t len,
+                             npr_endianness endianness, npr_record *out, size_t cap,
+                             size_t *n_out, size_t *consumed);
+/* CaptureFile::parse (src/file.rs:14-35) == net_parser_rs::parse (src/lib.rs:44-46). */
+npr_status npr_capture_file_parse(npr_ctx *ctx, const uint8_t *input, size_t len,
+                                  npr_global_header *header, npr_record *out, size_t cap,
+                                  size_t *n_out, size_t *consumed);
+/* FlowExtraction::extract_flow (src/flow/mod.rs:20-48) for a batch of records: dense
+ * per-record status + flow (flow/flow_v6 rows of failed records are zero). `input` is the
+ * buffer the records' offsets index into. flows_v6 may be NULL. */
+npr_status npr_extract_flows(npr_ctx *ctx, const uint8_t *input, size_t len,
+                             const npr_record *records, size_t n, npr_flow *flows,
+                             npr_flow_v6 *flows_v6, uint8_t *status);
+/* flow::convert_records (src/flow/mod.rs:101-123): Ok flows in reverse record order.
+ * *n_out = number of flows (> cap => NPR_ERR_CAPACITY, nothing beyond cap written). */
+npr_status npr_convert_records(npr_ctx *ctx, const uint8_t *input, size_t len,
+                               const npr_record *records, size_t n, npr_flow *out,
+                               npr_flow_v6 *out_v6, size_t cap, size_t *n_out);
+/* The reference's `extract` bench step (benches/benches.rs:56-62) fused into one device
+ * pass: CaptureFile::parse + convert_records.  `records` (optional, may be NULL) receives
+ * the dense record table; `out`/`out_v6` the converted flows (left-aligned here). */
+npr_status npr_parse_extract(npr_ctx *ctx, const uint8_t *input, size_t len,
+                             npr_global_header *header, npr_record *records, size_t record_cap,
+                             size_t *n_records, npr_flow *out, npr_flow_v6 *out_v6,
+                             size_t flow_cap, size_t *n_flows, size_t *consumed);
+
+/* ---- device-resident entry points ------------------------------------------------------- */
+/* The hot path: one launch finds the record chain starting at `start` (24 for a capture
+ * file, 0 for bare records), decodes every record and writes the outputs described in
+ * npr_dev_outputs.  `input` is a 16-byte-aligned device pointer; `stream` a hipStream_t
+ * (NULL = the context's stream).  Asynchronous: read `summary` after the stream syncs,
+ * or call npr_dev_check() which also reports NPR_ERR_CAPACITY / NPR_ERR_TIMEOUT. */
+npr_status npr_dev_parse_extract(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
+                                 npr_endianness endianness, const npr_dev_outputs *out,
+                                 void *stream);
+/* Synchronise `stream`, copy the summary back and map its flags to a status. */
+npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
+                         npr_summary *host_summary);
+/* Dense extract_flow over device-resident records (device npr_record array indexing into
+ * `input`; payload = input[offset+16 .. offset+16+actual_length]). */
+npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
+                                 const npr_record *records, uint64_t n, npr_flow *flows,
+                                 npr_flow_v6 *flows_v6, uint8_t *status, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NPR_H */

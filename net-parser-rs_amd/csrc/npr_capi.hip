@@ -1,0 +1,394 @@
+// npr_capi.hip — the C-ABI (include/npr.h) over the gfx950 kernels in npr_kernels.hip.
+//
+// Host-side single-object parsers (GlobalHeader::parse, PcapRecord::parse: 24 / 16 bytes) run
+// on the CPU by design; every multi-record path runs on the device.  There is no CPU fallback:
+// without a HIP device npr_ctx_create fails.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "../../include/npr.h"
+#include "npr_internal.hpp"
+
+#define NPR_VERSION_STRING "net-parser-rs_amd 0.1.0 (gfx950)"
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+};
+
+struct npr_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf slots;            // npr::TileSlot[]
+  uint32_t epoch = 0;      // last granule tag used (1..65535)
+  uint32_t *abort_word = nullptr;
+  npr_summary *summary = nullptr;   // device
+  npr_summary *summary_h = nullptr; // pinned host
+  // staging for the host-memory entry points
+  DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
+  std::string err;
+};
+
+namespace {
+
+constexpr uint32_t kTimeoutTicks = 100u * 1000u * 1000u;  // 1 s of s_memrealtime (100 MHz)
+
+npr_status fail(npr_ctx *c, npr_status st, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (c) c->err = buf;
+  return st;
+}
+
+#define HIP_CHECK(c, expr)                                                                 \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail((c), NPR_ERR_DEVICE, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_),     \
+                  __FILE__, __LINE__);                                                     \
+  } while (0)
+
+npr_status ensure(npr_ctx *c, DevBuf &b, size_t bytes, bool zero = false) {
+  if (bytes == 0) bytes = 16;
+  if (b.cap >= bytes) return NPR_OK;
+  if (b.p) {
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    HIP_CHECK(c, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+  }
+  size_t want = std::max(bytes, b.cap + b.cap / 2);
+  want = (want + 4095) & ~(size_t)4095;
+  HIP_CHECK(c, hipMalloc(&b.p, want));
+  if (zero) {  // visible to launches on any stream: finish it here (allocation is rare)
+    HIP_CHECK(c, hipMemsetAsync(b.p, 0, want, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  }
+  b.cap = want;
+  return NPR_OK;
+}
+
+inline uint32_t rd_u32(const uint8_t *p, bool big) {
+  uint32_t v;
+  memcpy(&v, p, 4);
+  return big ? __builtin_bswap32(v) : v;
+}
+inline uint16_t rd_u16(const uint8_t *p, bool big) {
+  uint16_t v;
+  memcpy(&v, p, 2);
+  return big ? (uint16_t)__builtin_bswap16(v) : v;
+}
+
+uint64_t tiles_for(uint64_t len, uint64_t start, uint64_t *org_out) {
+  const uint64_t org = start - start % npr::kTile;
+  if (org_out) *org_out = org;
+  const uint64_t span = len > org ? len - org : 0;
+  const uint64_t nt = (span + npr::kTile - 1) / npr::kTile;
+  return nt ? nt : 1;
+}
+
+hipStream_t pick(npr_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+}  // namespace
+
+extern "C" {
+
+const char *npr_version(void) { return NPR_VERSION_STRING; }
+int npr_abi_version(void) { return NPR_ABI_VERSION; }
+
+uint64_t npr_workspace_bytes(uint64_t len) {
+  return tiles_for(len, 0, nullptr) * sizeof(npr::TileSlot);
+}
+
+npr_status npr_ctx_create(int device, npr_ctx **out) {
+  if (!out) return NPR_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) return NPR_ERR_DEVICE;
+  npr_ctx *c = new npr_ctx();
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc((void **)&c->abort_word, 64) != hipSuccess || hipMalloc((void **)&c->summary, sizeof(npr_summary)) != hipSuccess ||
+      hipHostMalloc((void **)&c->summary_h, sizeof(npr_summary), 0) != hipSuccess ||
+      hipMemset(c->abort_word, 0, 64) != hipSuccess) {
+    npr_ctx_destroy(c);
+    return NPR_ERR_DEVICE;
+  }
+  *out = c;
+  return NPR_OK;
+}
+
+void npr_ctx_destroy(npr_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (DevBuf *b : {&c->slots, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+                    &c->flows2_v6, &c->scratch})
+    if (b->p) (void)hipFree(b->p);
+  if (c->abort_word) (void)hipFree(c->abort_word);
+  if (c->summary) (void)hipFree(c->summary);
+  if (c->summary_h) (void)hipHostFree(c->summary_h);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+const char *npr_ctx_last_error(const npr_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+// ---- GlobalHeader::parse (src/global_header.rs:40-70) ----------------------------------------
+npr_status npr_global_header_parse(const uint8_t *in, size_t len, npr_global_header *out, size_t *consumed) {
+  if (!out || (!in && len)) return NPR_ERR_ARG;
+  if (len < 24) return NPR_INCOMPLETE;  // every field is a fixed-width nom primitive
+  uint32_t magic;
+  memcpy(&magic, in, 4);  // u32!(NATIVE_ENDIAN), little-endian host
+  const bool big = magic != 0xA1B2C3D4u;  // == MAGIC => native (Little), else Big (:43-53)
+  out->endianness = big ? NPR_BIG : NPR_LITTLE;
+  out->version_major = rd_u16(in + 4, big);
+  out->version_minor = rd_u16(in + 6, big);
+  out->zone = (int32_t)rd_u32(in + 8, big);
+  out->sig_figs = (int32_t)rd_u32(in + 12, big);
+  out->snap_length = rd_u32(in + 16, big);
+  out->network = rd_u32(in + 20, big);
+  if (consumed) *consumed = 24;
+  return NPR_OK;
+}
+
+// ---- PcapRecord::parse (src/record.rs:102-121) ------------------------------------------------
+npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr_record *out, size_t *consumed) {
+  if (!out || (!in && len)) return NPR_ERR_ARG;
+  if (len < 16) return NPR_INCOMPLETE;
+  const bool big = e == NPR_BIG;
+  const uint32_t incl = rd_u32(in + 8, big);
+  if (len - 16 < incl) return NPR_INCOMPLETE;  // take!(actual_length)
+  out->offset = 0;
+  out->ts_sec = rd_u32(in, big);
+  out->ts_usec = rd_u32(in + 4, big);
+  out->actual_length = incl;
+  out->original_length = rd_u32(in + 12, big);
+  if (consumed) *consumed = 16 + (size_t)incl;
+  return NPR_OK;
+}
+
+// ---- device-resident hot path -----------------------------------------------------------------
+npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
+                                 npr_endianness e, const npr_dev_outputs *o, void *stream) {
+  if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
+  if (o->flows && (((uintptr_t)o->flows & 15u) != 0 || (o->flows_v6 && ((uintptr_t)o->flows_v6 & 15u))))
+    return fail(c, NPR_ERR_ARG, "flow arrays must be 16-byte aligned");
+  if (len >= (1ull << 40)) return fail(c, NPR_ERR_ARG, "input larger than 1 TiB (40-bit record offsets)");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  uint64_t org = 0;
+  const uint64_t nt = tiles_for(len, start, &org);
+  if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
+  npr_status st = ensure(c, c->slots, nt * sizeof(npr::TileSlot), true);
+  if (st) return st;
+  hipStream_t s = pick(c, stream);
+  if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
+    c->epoch = 1;
+    HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
+    HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, 64, s));
+  }
+  npr::ParseParams p{};
+  p.buf = (const uint8_t *)input;
+  p.len = len;
+  p.start = start;
+  p.org = org;
+  p.big = e == NPR_BIG;
+  p.epoch = c->epoch;
+  p.ntiles = (uint32_t)nt;
+  p.frac_max = 1000000000u;
+  p.flags = 0;
+  p.timeout_ticks = kTimeoutTicks;
+  p.slots = (npr::TileSlot *)c->slots.p;
+  p.abort_word = c->abort_word;
+  p.rec_off = o->record_offsets;
+  p.recs = o->records;
+  p.rec_status = o->record_status;
+  p.rec_cap = o->record_cap;
+  p.flows = (uint32_t *)o->flows;
+  p.flows_v6 = (uint32_t *)o->flows_v6;
+  p.flow_cap = o->flow_cap;
+  p.summary = o->summary;
+  HIP_CHECK(c, npr::launch_parse_extract(p, s));
+  return NPR_OK;
+}
+
+npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr_summary *hs) {
+  if (!c || !o || !o->summary) return NPR_ERR_ARG;
+  hipStream_t s = pick(c, stream);
+  HIP_CHECK(c, hipMemcpyAsync(c->summary_h, o->summary, sizeof(npr_summary), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  if (hs) *hs = *c->summary_h;
+  if (c->summary_h->epoch != c->epoch)
+    return fail(c, NPR_ERR_TIMEOUT, "parse did not complete (tile hand-off timed out)");
+  if (c->summary_h->flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded (flags=%u)", c->summary_h->flags);
+  return NPR_OK;
+}
+
+npr_status npr_dev_extract_flows(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs,
+                                 uint64_t n, npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status,
+                                 void *stream) {
+  if (!c || (!input && len) || (!recs && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  HIP_CHECK(c, npr::launch_extract_dense((const uint8_t *)input, len, recs, n, (uint32_t *)flows,
+                                         (uint32_t *)flows_v6, status, pick(c, stream)));
+  return NPR_OK;
+}
+
+// ---- host-memory entry points ---------------------------------------------------------------
+static npr_status stage_input(npr_ctx *c, const uint8_t *in, size_t len) {
+  npr_status st = ensure(c, c->in, len + 16);
+  if (st) return st;
+  if (len) HIP_CHECK(c, hipMemcpyAsync(c->in.p, in, len, hipMemcpyHostToDevice, c->stream));
+  return NPR_OK;
+}
+
+// Shared body of records_parse / capture_file_parse / parse_extract.
+static npr_status host_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64_t start, npr_endianness e,
+                             npr_record *out_recs, size_t rec_cap, size_t *n_records, npr_flow *out_flows,
+                             npr_flow_v6 *out_v6, size_t flow_cap, size_t *n_flows, size_t *consumed) {
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = stage_input(c, in, len);
+  if (st) return st;
+  const uint64_t max_rec = len > start ? (len - start) / 16 + 1 : 1;
+  const uint64_t rcap = std::min<uint64_t>(rec_cap, max_rec);
+  const uint64_t fcap = std::min<uint64_t>(flow_cap, max_rec);
+  npr_dev_outputs o{};
+  if (out_recs && rcap) {
+    if ((st = ensure(c, c->recs, rcap * sizeof(npr_record)))) return st;
+    o.records = (npr_record *)c->recs.p;
+    o.record_cap = rcap;
+  }
+  if (out_flows && fcap) {
+    if ((st = ensure(c, c->flows, fcap * sizeof(npr_flow)))) return st;
+    o.flows = (npr_flow *)c->flows.p;
+    o.flow_cap = fcap;
+    if (out_v6) {
+      if ((st = ensure(c, c->flows_v6, fcap * sizeof(npr_flow_v6)))) return st;
+      o.flows_v6 = (npr_flow_v6 *)c->flows_v6.p;
+    }
+  }
+  o.summary = c->summary;
+  if ((st = npr_dev_parse_extract(c, c->in.p, len, start, e, &o, c->stream))) return st;
+  npr_summary sm;
+  st = npr_dev_check(c, &o, c->stream, &sm);
+  if (st && st != NPR_ERR_CAPACITY) return st;
+  const uint64_t nr = std::min<uint64_t>(sm.n_records, rcap);
+  const uint64_t nf = std::min<uint64_t>(sm.n_flows, fcap);
+  if (o.records && nr)
+    HIP_CHECK(c, hipMemcpyAsync(out_recs, o.records, nr * sizeof(npr_record), hipMemcpyDeviceToHost, c->stream));
+  if (o.flows && nf) {  // device flows are right-aligned; the host API returns them left-aligned
+    HIP_CHECK(c, hipMemcpyAsync(out_flows, o.flows + (fcap - nf), nf * sizeof(npr_flow), hipMemcpyDeviceToHost,
+                                c->stream));
+    if (o.flows_v6)
+      HIP_CHECK(c, hipMemcpyAsync(out_v6, o.flows_v6 + (fcap - nf), nf * sizeof(npr_flow_v6),
+                                  hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  if (n_records) *n_records = sm.n_records;
+  if (n_flows) *n_flows = sm.n_flows;
+  if (consumed) *consumed = sm.consumed;
+  if ((out_recs && sm.n_records > rec_cap) || (out_flows && sm.n_flows > flow_cap))
+    return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+  return NPR_OK;
+}
+
+npr_status npr_records_parse(npr_ctx *c, const uint8_t *in, size_t len, npr_endianness e, npr_record *out,
+                             size_t cap, size_t *n_out, size_t *consumed) {
+  if (!c || (!in && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  return host_parse(c, in, len, 0, e, out, out ? cap : 0, n_out, nullptr, nullptr, 0, nullptr, consumed);
+}
+
+npr_status npr_capture_file_parse(npr_ctx *c, const uint8_t *in, size_t len, npr_global_header *hdr,
+                                  npr_record *out, size_t cap, size_t *n_out, size_t *consumed) {
+  if (!c || !hdr || (!in && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  npr_status st = npr_global_header_parse(in, len, hdr, nullptr);  // file.rs:18
+  if (st) return st;
+  return host_parse(c, in, len, 24, (npr_endianness)hdr->endianness, out, out ? cap : 0, n_out, nullptr,
+                    nullptr, 0, nullptr, consumed);
+}
+
+npr_status npr_parse_extract(npr_ctx *c, const uint8_t *in, size_t len, npr_global_header *hdr, npr_record *recs,
+                             size_t rec_cap, size_t *n_records, npr_flow *out, npr_flow_v6 *out_v6, size_t flow_cap,
+                             size_t *n_flows, size_t *consumed) {
+  if (!c || !hdr || (!in && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  npr_status st = npr_global_header_parse(in, len, hdr, nullptr);
+  if (st) return st;
+  return host_parse(c, in, len, 24, (npr_endianness)hdr->endianness, recs, recs ? rec_cap : 0, n_records, out,
+                    out_v6, out ? flow_cap : 0, n_flows, consumed);
+}
+
+npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const npr_record *records, size_t n,
+                             npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status) {
+  if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = stage_input(c, in, len);
+  if (st) return st;
+  if (n == 0) return NPR_OK;
+  if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
+  if ((st = ensure(c, c->flows, n * sizeof(npr_flow)))) return st;
+  if ((st = ensure(c, c->flows_v6, n * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->status, n))) return st;
+  HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, npr::launch_extract_dense((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n,
+                                         (uint32_t *)c->flows.p, (uint32_t *)c->flows_v6.p, (uint8_t *)c->status.p,
+                                         c->stream));
+  if (flows) HIP_CHECK(c, hipMemcpyAsync(flows, c->flows.p, n * sizeof(npr_flow), hipMemcpyDeviceToHost, c->stream));
+  if (flows_v6)
+    HIP_CHECK(c, hipMemcpyAsync(flows_v6, c->flows_v6.p, n * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
+  if (status) HIP_CHECK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  return NPR_OK;
+}
+
+npr_status npr_convert_records(npr_ctx *c, const uint8_t *in, size_t len, const npr_record *records, size_t n,
+                               npr_flow *out, npr_flow_v6 *out_v6, size_t cap, size_t *n_out) {
+  if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = stage_input(c, in, len);
+  if (st) return st;
+  if (n == 0) {
+    if (n_out) *n_out = 0;
+    return NPR_OK;
+  }
+  const uint64_t ocap = std::min<uint64_t>(cap, n);
+  if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
+  if ((st = ensure(c, c->flows, n * sizeof(npr_flow)))) return st;
+  if ((st = ensure(c, c->flows_v6, n * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->status, n))) return st;
+  if ((st = ensure(c, c->flows2, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow)))) return st;
+  if ((st = ensure(c, c->flows2_v6, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->scratch, npr::compact_workspace_words(n) * 4 + 64))) return st;
+  HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, npr::launch_extract_dense((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n,
+                                         (uint32_t *)c->flows.p, (uint32_t *)c->flows_v6.p, (uint8_t *)c->status.p,
+                                         c->stream));
+  uint64_t *total = (uint64_t *)c->summary;  // scratch word
+  HIP_CHECK(c, npr::launch_compact_reverse((const uint32_t *)c->flows.p, (const uint32_t *)c->flows_v6.p,
+                                           (const uint8_t *)c->status.p, n, (uint32_t *)c->flows2.p,
+                                           (uint32_t *)c->flows2_v6.p, ocap, (uint32_t *)c->scratch.p, total,
+                                           c->stream));
+  uint64_t tot = 0;
+  HIP_CHECK(c, hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  const uint64_t k = std::min<uint64_t>(tot, ocap);
+  if (k) {
+    if (out) HIP_CHECK(c, hipMemcpyAsync(out, c->flows2.p, k * sizeof(npr_flow), hipMemcpyDeviceToHost, c->stream));
+    if (out_v6)
+      HIP_CHECK(c, hipMemcpyAsync(out_v6, c->flows2_v6.p, k * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  }
+  if (n_out) *n_out = tot;
+  if (tot > cap) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+  return NPR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,150 @@
+"""ctypes / numpy view of include/npr.h (the C-ABI of libnpr.so).
+
+Loading is strict: if the HIP library is missing this raises instead of falling back to
+anything else — there is no CPU path in the product.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)                 # net-parser-rs_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libnpr.so")
+
+# ---- numpy record dtypes (byte-for-byte the C structs) ----------------------------------
+RECORD_DTYPE = np.dtype(
+    [("offset", "<u8"), ("ts_sec", "<u4"), ("ts_usec", "<u4"),
+     ("actual_length", "<u4"), ("original_length", "<u4")], align=True)
+FLOW_DTYPE = np.dtype(
+    [("src_ip", "u1", (4,)), ("dst_ip", "u1", (4,)), ("src_port", "<u2"), ("dst_port", "<u2"),
+     ("vlan", "<u2"), ("src_mac", "u1", (6,)), ("dst_mac", "u1", (6,)), ("kind", "u1"),
+     ("record_offset", "u1", (5,))], align=True)
+FLOW_V6_DTYPE = np.dtype([("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,))])
+SUMMARY_DTYPE = np.dtype([("n_records", "<u8"), ("n_flows", "<u8"), ("consumed", "<u8"),
+                          ("flags", "<u4"), ("epoch", "<u4")])
+assert RECORD_DTYPE.itemsize == 24 and FLOW_DTYPE.itemsize == 32 and FLOW_V6_DTYPE.itemsize == 32
+assert SUMMARY_DTYPE.itemsize == 32
+
+KIND_IPV6 = 0x1
+KIND_UDP = 0x2
+
+# npr_status
+OK, INCOMPLETE, FAILURE, CUSTOM = 0, 1, 2, 3
+ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
+LITTLE, BIG = 0, 1
+
+# npr_flow_status (include/npr.h), name -> code
+FLOW_STATUS = {
+    "OK": 0, "ETH_INCOMPLETE": 1, "ETH_FAILURE": 2, "L2_ETHERTYPE": 3,
+    "L2_IPV4_INCOMPLETE": 4, "L2_IPV4_FAILURE": 5, "L2_IPV4_CUSTOM": 6,
+    "L2_IPV6_INCOMPLETE": 7, "L2_IPV6_FAILURE": 8, "L2_IPV6_CUSTOM": 9,
+    "L2_ARP_INCOMPLETE": 10, "L2_IPV4_REMAINDER": 11, "L2_IPV6_REMAINDER": 12,
+    "L2_ARP_REMAINDER": 13, "L3_ARP": 14, "L3_IPV4_PROTOCOL": 15, "L3_IPV6_PROTOCOL": 16,
+    "L3_IPV4_TCP_INCOMPLETE": 17, "L3_IPV4_TCP_FAILURE": 18, "L3_IPV4_UDP_INCOMPLETE": 19,
+    "L3_IPV6_TCP_INCOMPLETE": 20, "L3_IPV6_TCP_FAILURE": 21, "L3_IPV6_UDP_INCOMPLETE": 22,
+    "L3_IPV4_UDP_REMAINDER": 23, "L3_IPV6_UDP_REMAINDER": 24,
+}
+FLOW_STATUS_NAME = {v: k for k, v in FLOW_STATUS.items()}
+
+
+class GlobalHeaderC(ctypes.Structure):
+    _fields_ = [("endianness", ctypes.c_int32), ("version_major", ctypes.c_uint16),
+                ("version_minor", ctypes.c_uint16), ("zone", ctypes.c_int32),
+                ("sig_figs", ctypes.c_int32), ("snap_length", ctypes.c_uint32),
+                ("network", ctypes.c_uint32)]
+
+
+class RecordC(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("ts_sec", ctypes.c_uint32),
+                ("ts_usec", ctypes.c_uint32), ("actual_length", ctypes.c_uint32),
+                ("original_length", ctypes.c_uint32)]
+
+
+class DevOutputsC(ctypes.Structure):
+    _fields_ = [("record_offsets", ctypes.c_void_p), ("records", ctypes.c_void_p),
+                ("record_status", ctypes.c_void_p),
+                ("record_cap", ctypes.c_uint64), ("flows", ctypes.c_void_p),
+                ("flows_v6", ctypes.c_void_p), ("flow_cap", ctypes.c_uint64),
+                ("summary", ctypes.c_void_p)]
+
+
+class SummaryC(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("n_flows", ctypes.c_uint64),
+                ("consumed", ctypes.c_uint64), ("flags", ctypes.c_uint32),
+                ("epoch", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24
+
+# Every symbol include/npr.h declares (checked by tests/test_abi.py).
+EXPORTED = [
+    "npr_version", "npr_abi_version", "npr_ctx_create", "npr_ctx_destroy", "npr_ctx_last_error",
+    "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
+    "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
+    "npr_dev_parse_extract", "npr_dev_check", "npr_dev_extract_flows",
+]
+
+_c_size_p = ctypes.POINTER(ctypes.c_size_t)
+_vp = ctypes.c_void_p
+_u8p = ctypes.c_void_p
+
+_SIGNATURES = {
+    "npr_version": (ctypes.c_char_p, []),
+    "npr_abi_version": (ctypes.c_int, []),
+    "npr_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "npr_ctx_destroy": (None, [_vp]),
+    "npr_ctx_last_error": (ctypes.c_char_p, [_vp]),
+    "npr_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "npr_global_header_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _c_size_p]),
+    "npr_record_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(RecordC), _c_size_p]),
+    "npr_records_parse": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, ctypes.c_int, _vp, ctypes.c_size_t,
+                                         _c_size_p, _c_size_p]),
+    "npr_capture_file_parse": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _vp,
+                                              ctypes.c_size_t, _c_size_p, _c_size_p]),
+    "npr_extract_flows": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp, _vp]),
+    "npr_convert_records": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp,
+                                           ctypes.c_size_t, _c_size_p]),
+    "npr_parse_extract": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _vp,
+                                         ctypes.c_size_t, _c_size_p, _vp, _vp, ctypes.c_size_t, _c_size_p,
+                                         _c_size_p]),
+    "npr_dev_parse_extract": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                             ctypes.POINTER(DevOutputsC), _vp]),
+    "npr_dev_check": (ctypes.c_int, [_vp, ctypes.POINTER(DevOutputsC), _vp, ctypes.POINTER(SummaryC)]),
+    "npr_dev_extract_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                             _vp, _vp, _vp, _vp]),
+}
+
+_lib = None
+
+
+def load_library(path=None):
+    """Load libnpr.so (built by __graft_entry__.build()); raise loudly if it is absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise ImportError(
+            f"libnpr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the parser has no CPU fallback)")
+    lib = ctypes.CDLL(p)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def ptr(a):
+    """Address of a numpy array / bytes-like (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    if isinstance(a, (bytes, bytearray, memoryview)):
+        return np.frombuffer(a, dtype=np.uint8).ctypes.data
+    raise TypeError(type(a))

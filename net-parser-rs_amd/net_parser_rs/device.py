@@ -1,0 +1,103 @@
+"""Device-resident entry points over torch tensors (torch = HBM allocation + streams only).
+
+    ws = Workspace(record_cap, flow_cap, device=0)      # outputs allocated once, reused
+    ws.launch(buf, start=24, endianness=Endianness.Little)   # async, on the current torch stream
+    summary = ws.check()                                 # sync + totals / capacity errors
+
+`buf` is a contiguous uint8 CUDA tensor (16-byte aligned, as torch allocations are).  Outputs
+follow npr_dev_outputs (include/npr.h): dense record table / status in file order, flows in
+convert_records order RIGHT-aligned in [flow_cap - n_flows, flow_cap).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _abi, context
+
+
+class Workspace:
+    def __init__(self, record_cap, flow_cap, device=0, records=True, offsets=False, status=False,
+                 flows=True, flows_v6=True):
+        self.device = torch.device("cuda", device)
+        self.ctx = context(device)
+        self.record_cap, self.flow_cap = int(record_cap), int(flow_cap)
+        mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
+        self.records = mk(self.record_cap * 24) if records else None
+        self.offsets = mk(self.record_cap * 8) if offsets else None
+        self.status = mk(self.record_cap) if status else None
+        self.flows = mk(self.flow_cap * 32) if flows else None
+        self.flows_v6 = mk(self.flow_cap * 32) if flows_v6 else None
+        self.summary = torch.zeros(32, dtype=torch.uint8, device=self.device)
+        p = lambda t: t.data_ptr() if t is not None else None
+        self.outs = _abi.DevOutputsC(p(self.offsets), p(self.records), p(self.status), self.record_cap,
+                                     p(self.flows), p(self.flows_v6), self.flow_cap, p(self.summary))
+        self.last = None
+
+    def launch(self, buf, start=24, endianness=_abi.LITTLE, nbytes=None, stream=None):
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        n = buf.numel() if nbytes is None else int(nbytes)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        st = self.ctx.lib.npr_dev_parse_extract(self.ctx.handle, buf.data_ptr(), n, start, endianness,
+                                                ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        self.ctx.check(st)
+        self._stream = s
+
+    def check(self):
+        sm = _abi.SummaryC()
+        st = self.ctx.lib.npr_dev_check(self.ctx.handle, ctypes.byref(self.outs),
+                                        ctypes.c_void_p(self._stream.cuda_stream), ctypes.byref(sm))
+        self.last = sm
+        if st not in (_abi.OK,):
+            self.ctx.check(st)
+        return sm
+
+    # ---- host views of the results (for tests) ----
+    def records_np(self):
+        n = min(self.last.n_records, self.record_cap)
+        return self.records[: n * 24].cpu().numpy().view(_abi.RECORD_DTYPE)
+
+    def offsets_np(self):
+        n = min(self.last.n_records, self.record_cap)
+        return self.offsets[: n * 8].cpu().numpy().view("<u8")
+
+    def status_np(self):
+        n = min(self.last.n_records, self.record_cap)
+        return self.status[:n].cpu().numpy()
+
+    def flows_np(self):
+        k = min(self.last.n_flows, self.flow_cap)
+        return self.flows[(self.flow_cap - k) * 32: self.flow_cap * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+
+    def flows_v6_np(self):
+        k = min(self.last.n_flows, self.flow_cap)
+        return self.flows_v6[(self.flow_cap - k) * 32: self.flow_cap * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
+
+
+class Result:
+    def __init__(self, ws, sm):
+        self.ws = ws
+        self.n_records, self.n_flows, self.consumed, self.flags = sm.n_records, sm.n_flows, sm.consumed, sm.flags
+
+    def records_np(self):
+        return self.ws.records_np()
+
+    def status_np(self):
+        return self.ws.status_np()
+
+    def flows_np(self):
+        return self.ws.flows_np()
+
+    def flows_v6_np(self):
+        return self.ws.flows_v6_np()
+
+
+def parse_extract(buf, start=24, endianness=_abi.LITTLE, record_cap=None, flow_cap=None, status=True):
+    """One-shot device parse + extract + convert over a CUDA uint8 tensor (sync)."""
+    n = buf.numel()
+    cap = max((n - start) // 16 + 1, 1) if n > start else 1
+    ws = Workspace(record_cap if record_cap is not None else cap, flow_cap if flow_cap is not None else cap,
+                   device=buf.device.index or 0, status=status)
+    ws.launch(buf, start=start, endianness=endianness)
+    sm = ws.check()
+    return Result(ws, sm)

@@ -1,0 +1,139 @@
+"""net_parser_rs.flow — mirror of src/flow/ (Flow, Device, errors, convert_records) over libnpr.so."""
+import ctypes
+import ipaddress
+
+import numpy as np
+
+from . import _abi
+
+__all__ = ["Flow", "Device", "MacAddress", "FlowError", "convert_records", "FlowExtraction"]
+
+
+class MacAddress(bytes):
+    """common::MacAddress (src/common.rs:3-26)."""
+
+    def __str__(self):
+        return ":".join(f"{b:02x}" for b in self)
+
+
+class Device:
+    """flow::device::Device (src/flow/device.rs:7-27)."""
+    __slots__ = ("mac", "ip", "port")
+
+    def __init__(self, mac, ip, port):
+        self.mac, self.ip, self.port = MacAddress(mac), ip, int(port)
+
+    def __eq__(self, o):
+        return isinstance(o, Device) and (self.mac, self.ip, self.port) == (o.mac, o.ip, o.port)
+
+    def __str__(self):
+        return f"Mac={self.mac}   Ip={_ip_str(self.ip)}   Port={self.port}"
+
+
+def _ip_str(ip):
+    if isinstance(ip, ipaddress.IPv6Address):
+        return str(ip)  # RFC 5952 form, as std::net::Ipv6Addr's Display for ordinary addresses
+    return str(ip)
+
+
+class Flow:
+    """flow::Flow (src/flow/mod.rs:53-96).  layer2 is always "Ethernet"."""
+    __slots__ = ("source", "destination", "layer2", "layer3", "layer4", "vlan", "record_offset")
+
+    def __init__(self, source, destination, layer3, layer4, vlan, layer2="Ethernet", record_offset=None):
+        self.source, self.destination = source, destination
+        self.layer2, self.layer3, self.layer4, self.vlan = layer2, layer3, layer4, int(vlan)
+        self.record_offset = record_offset
+
+    def __eq__(self, o):
+        return isinstance(o, Flow) and (self.source, self.destination, self.layer2, self.layer3, self.layer4,
+                                        self.vlan) == (o.source, o.destination, o.layer2, o.layer3, o.layer4, o.vlan)
+
+    def __str__(self):
+        return f"Source=[{self.source}]   Destination=[{self.destination}]   Vlan={self.vlan}"
+
+    @staticmethod
+    def _from_row(row, v6row=None):
+        kind = int(row["kind"])
+        if kind & _abi.KIND_IPV6:
+            src = ipaddress.IPv6Address(bytes(v6row["src_ip"]))
+            dst = ipaddress.IPv6Address(bytes(v6row["dst_ip"]))
+        else:
+            src = ipaddress.IPv4Address(bytes(row["src_ip"]))
+            dst = ipaddress.IPv4Address(bytes(row["dst_ip"]))
+        off = int.from_bytes(bytes(row["record_offset"]), "little")
+        return Flow(Device(bytes(row["src_mac"]), src, row["src_port"]),
+                    Device(bytes(row["dst_mac"]), dst, row["dst_port"]),
+                    "IPv6" if kind & _abi.KIND_IPV6 else "IPv4",
+                    "Udp" if kind & _abi.KIND_UDP else "Tcp", row["vlan"], record_offset=off)
+
+
+class FlowError(Exception):
+    """flow::errors::Error (src/flow/errors.rs:5-19); `.code` is the npr_flow_status leaf."""
+
+    def __init__(self, code):
+        self.code = int(code)
+        self.name = _abi.FLOW_STATUS_NAME.get(self.code, f"UNKNOWN_{code}")
+        super().__init__(self.name)
+
+
+def _table(records):
+    t = np.zeros(len(records), dtype=_abi.RECORD_DTYPE)
+    for i, r in enumerate(records):
+        t[i] = (r.offset, r.ts_sec, r.ts_usec, r.actual_length, r.original_length)
+    return t
+
+
+def _extract(buf, records):
+    """Dense extract over records that all index into `buf` (one device launch)."""
+    from . import context
+    ctx = context()
+    a = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    t = _table(records)
+    n = len(t)
+    flows = np.zeros(max(n, 1), dtype=_abi.FLOW_DTYPE)
+    v6 = np.zeros(max(n, 1), dtype=_abi.FLOW_V6_DTYPE)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    ctx.check(ctx.lib.npr_extract_flows(ctx.handle, a.ctypes.data if a.size else None, a.size, t.ctypes.data, n,
+                                        flows.ctypes.data, v6.ctypes.data, status.ctypes.data))
+    return flows[:n], v6[:n], status[:n]
+
+
+def convert_records(records):
+    """flow::convert_records (src/flow/mod.rs:101-123): [(record, Flow)] for Ok records, in REVERSE
+    record order (the reference pops from the end)."""
+    from . import context
+    records = list(records)
+    if not records:
+        return []
+    # group by backing buffer (records from one parse share it); keep the global reverse order
+    out = []
+    bufs = {}
+    for r in records:
+        bufs.setdefault(id(r._buf), r._buf)
+    if len(bufs) == 1:
+        buf = next(iter(bufs.values()))
+        ctx = context()
+        a = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+        t = _table(records)
+        n = len(t)
+        flows = np.zeros(n, dtype=_abi.FLOW_DTYPE)
+        v6 = np.zeros(n, dtype=_abi.FLOW_V6_DTYPE)
+        k = ctypes.c_size_t(0)
+        ctx.check(ctx.lib.npr_convert_records(ctx.handle, a.ctypes.data if a.size else None, a.size, t.ctypes.data,
+                                              n, flows.ctypes.data, v6.ctypes.data, n, ctypes.byref(k)))
+        by_off = {r.offset: r for r in records}
+        for i in range(k.value):
+            f = Flow._from_row(flows[i], v6[i])
+            out.append((by_off[f.record_offset], f))
+        return out
+    for r in reversed(records):
+        try:
+            out.append((r, r.extract_flow()))
+        except FlowError:
+            pass
+    return out
+
+
+class FlowExtraction:
+    """Trait marker (src/flow/mod.rs:20-42): PcapRecord implements extract_flow()."""

@@ -1,0 +1,118 @@
+"""CPU-side checks of the C-ABI: the library loads, exports every symbol include/npr.h declares,
+struct layouts agree, and the host-side single-object parsers match the reference KATs."""
+import json
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import net_parser_rs as npr
+from net_parser_rs import _abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KATS = {k["name"]: k for k in json.load(open(os.path.join(REPO, "tests", "golden", "kat.json")))["kats"]}
+
+
+def declared_symbols():
+    src = open(os.path.join(REPO, "include", "npr.h")).read()
+    return sorted(set(re.findall(r"\b(npr_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_what_abi_lists():
+    assert declared_symbols() == sorted(_abi.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _abi.load_library()
+    for s in declared_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (npr_\w+)", out))
+    assert set(declared_symbols()) <= exported
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle target id
+
+
+def test_struct_sizes_match_c():
+    code = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "npr.h"
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_header), sizeof(npr_record),
+ sizeof(npr_flow), sizeof(npr_flow_v6), sizeof(npr_summary), sizeof(npr_dev_outputs),
+ offsetof(npr_flow, kind), offsetof(npr_flow, record_offset)); return 0;}'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(code)
+        subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), c, "-o", os.path.join(d, "t")],
+                       check=True)
+        vals = list(map(int, subprocess.run([os.path.join(d, "t")], capture_output=True, text=True).stdout.split()))
+    assert vals == [24, 24, 32, 32, 32, 64, _abi.FLOW_DTYPE.fields["kind"][1],
+                    _abi.FLOW_DTYPE.fields["record_offset"][1]]
+    import ctypes
+    assert ctypes.sizeof(_abi.DevOutputsC) == 64
+
+
+def test_abi_version():
+    lib = _abi.load_library()
+    assert lib.npr_abi_version() == 1
+    assert b"gfx950" in lib.npr_version()
+
+
+@pytest.mark.parametrize("name", ["global_header_native_endian", "global_header_not_native_endian"])
+def test_global_header_kat_via_product(name):
+    k = KATS[name]
+    rem, h = npr.GlobalHeader.parse(bytes.fromhex(k["input"]))
+    e = k["expect"]
+    assert len(rem) == e["rem"]
+    assert h.endianness == (npr.Endianness.Big if e["endianness"] == "big" else npr.Endianness.Little)
+    assert (h.version_major, h.version_minor, h.snap_length) == (e["version_major"], e["version_minor"],
+                                                                e["snap_length"])
+
+
+def test_record_kats_via_product():
+    k = KATS["parse_record"]
+    rem, r = npr.PcapRecord.parse(bytes.fromhex(k["input"]), npr.Endianness.Big)
+    e = k["expect"]
+    assert len(rem) == 0
+    assert (r.ts_sec, r.ts_usec, r.actual_length, r.original_length) == (
+        e["ts_sec"], e["ts_usec"], e["actual_length"], e["original_length"])
+    assert str(r) == KATS["display_record"]["expect"]["display"]
+    assert npr.PcapRecord.convert_packet_time(1527868899, 152053) == KATS["convert_timestamp"]["expect"]["timestamp_ns"]
+
+
+def test_short_inputs_are_incomplete():
+    with pytest.raises(npr.Incomplete):
+        npr.GlobalHeader.parse(b"\xd4\xc3\xb2\xa1" + bytes(10))
+    with pytest.raises(npr.Incomplete):
+        npr.PcapRecord.parse(bytes(15), npr.Endianness.Little)
+    with pytest.raises(npr.Incomplete):  # take!(actual_length) past the end
+        npr.PcapRecord.parse(bytes(8) + (100).to_bytes(4, "little") + bytes(4) + bytes(50), npr.Endianness.Little)
+
+
+def test_display_strings():
+    from net_parser_rs import flow
+    import ipaddress
+    k = KATS["format_flow"]["flow"]
+    f = flow.Flow(flow.Device(bytes.fromhex(k["src_mac"].replace(":", "")), ipaddress.ip_address(k["src_ip"]), k["src_port"]),
+                  flow.Device(bytes.fromhex(k["dst_mac"].replace(":", "")), ipaddress.ip_address(k["dst_ip"]), k["dst_port"]),
+                  "IPv4", "Tcp", k["vlan"])
+    assert str(f) == KATS["format_flow"]["expect"]["display"]
+    d = KATS["format_device"]["device"]
+    dev = flow.Device(bytes.fromhex(d["mac"].replace(":", "")), ipaddress.ip_address(d["ip"]), d["port"])
+    assert str(dev) == KATS["format_device"]["expect"]["display"]
+    assert str(flow.MacAddress(bytes.fromhex(KATS["format_mac_address"]["input"]))) == "00:01:02:03:04:05"
+
+
+def test_device_call_without_gpu_fails_loudly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(npr.DeviceError):
+        npr.CaptureFile.parse(bytes.fromhex(KATS["file_bytes_parse"]["input"]))

@@ -1,0 +1,227 @@
+"""Parity of the HIP path (through the C-ABI) against the CPU oracle, bit-exact.
+
+Every case runs the fused device kernel (npr_dev_parse_extract) and compares: the record table
+(offset, ts, lengths), per-record flow status, the convert_records flow table (bytes, incl. IPv6
+side table), n_records / n_flows and `consumed` (the Rust remainder).  Inputs are seeded
+synthetic captures (net_parser_rs.synth) sized so the oracle finishes in seconds, plus the
+reference's own KAT frames.  Full-size configs are checked through properties (test_gpu_full.py).
+"""
+import json
+import os
+import struct
+
+import numpy as np
+import pytest
+import torch
+
+import _oracle
+import net_parser_rs as npr
+from net_parser_rs import _abi, device, synth
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KATS = {k["name"]: k for k in json.load(open(os.path.join(REPO, "tests", "golden", "kat.json")))["kats"]}
+
+
+def to_dev(blob):
+    t = torch.empty(max(len(blob), 1), dtype=torch.uint8, device="cuda")
+    if blob:
+        t[: len(blob)].copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
+    return t[: len(blob)] if blob else t[:0]
+
+
+def check_parity(blob, start=24, endianness=None, ws=None):
+    """Run the device path on `blob` and compare everything with the oracle."""
+    if start == 24:
+        rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
+        assert rc == 0
+        e = hdr.endianness if endianness is None else endianness
+    else:
+        e = endianness
+        want_recs, cons = _oracle.records_parse(blob[start:], e)
+        want_recs = want_recs.copy()
+        want_recs["offset"] += start
+        want_cons = start + cons
+    want_flows, want_v6 = _oracle.convert_records(blob, want_recs)
+    _, _, want_status = _oracle.extract_flows(blob, want_recs)
+    buf = to_dev(blob)
+    n = len(blob)
+    cap = max((n - start) // 16 + 1, 1)
+    w = ws or device.Workspace(cap, cap, status=True)
+    w.launch(buf, start=start, endianness=e, nbytes=n)
+    sm = w.check()
+    assert sm.n_records == len(want_recs), (sm.n_records, len(want_recs))
+    assert sm.consumed == want_cons, (sm.consumed, want_cons)
+    assert sm.n_flows == len(want_flows)
+    got_recs = w.records_np()
+    assert got_recs.tobytes() == want_recs.tobytes(), first_diff(got_recs, want_recs)
+    got_status = w.status_np()
+    assert np.array_equal(got_status, want_status), first_diff(got_status, want_status)
+    got_flows = w.flows_np()
+    assert got_flows.tobytes() == want_flows.tobytes(), first_diff(got_flows, want_flows)
+    v6mask = (want_flows["kind"] & _abi.KIND_IPV6) != 0
+    if v6mask.any():
+        assert w.flows_v6_np()[v6mask].tobytes() == want_v6[v6mask].tobytes()
+    return sm
+
+
+def first_diff(a, b):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if a[i].tobytes() != b[i].tobytes():
+            return f"first diff at {i}: got {a[i]} want {b[i]} (len {len(a)} vs {len(b)})"
+    return f"lengths {len(a)} vs {len(b)}"
+
+
+# ---- the reference's own vectors through the device ------------------------------------------
+def test_kat_file_bytes_parse_big_endian():
+    blob = bytes.fromhex(KATS["file_bytes_parse"]["input"])
+    sm = check_parity(blob)
+    assert sm.n_records == 1 and sm.consumed == len(blob) and sm.n_flows == 1
+    rem, f = npr.CaptureFile.parse(blob)  # the mirror API (host memory in, host memory out)
+    assert len(rem) == 0 and f.global_header.endianness == npr.Endianness.Big and f.records.len() == 1
+    rec = f.records.into_inner()[0]
+    fl = rec.extract_flow()
+    assert (fl.source.port, fl.destination.port) == (50871, 80)
+    pairs = npr.flow.convert_records(f.records.into_inner())
+    assert len(pairs) == 1 and pairs[0][1] == fl
+
+
+@pytest.mark.parametrize("name", ["convert_ethernet_tcp", "encapsulated", "not_encapsulated",
+                                  "parse_ethernet_payload"])
+def test_kat_frames_as_records(name):
+    frame = bytes.fromhex(KATS[name]["input"])
+    blob = synth.global_header() + struct.pack("<IIII", 1, 2, len(frame), len(frame)) + frame
+    check_parity(blob)
+
+
+# ---- synthetic corpora ---------------------------------------------------------------------
+def test_c2_small():
+    check_parity(synth.fixed64(50_000))
+
+
+def test_c3_small():
+    check_parity(synth.variable_mix(20_000))
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_quirk_corpus(seed):
+    check_parity(synth.quirk_corpus(8_000, seed=seed))
+
+
+def test_quirk_corpus_big_endian():
+    check_parity(synth.quirk_corpus(6_000, seed=11, big=True))
+
+
+def test_adversarial_speculation():
+    """Fake record-header chains inside payloads, zero-filled payloads and jumbo (> tile) records
+    defeat the per-tile start speculation; the look-back must still reproduce the serial chain."""
+    check_parity(synth.quirk_corpus(4_000, seed=5, fake_every=3, zero_every=7, jumbo_every=200))
+
+
+def test_jumbo_records_span_many_tiles():
+    check_parity(synth.quirk_corpus(600, seed=6, jumbo_every=2))
+
+
+@pytest.mark.parametrize("tail", ["truncated_header", "truncated_payload", "huge_incl"])
+def test_truncated_tails(tail):
+    sm = check_parity(synth.quirk_corpus(3_000, seed=9, tail=tail))
+    assert sm.consumed < len(synth.quirk_corpus(3_000, seed=9, tail=tail))
+
+
+def test_corrupt_incl_mid_file_stops_chain():
+    blob = synth.corrupt_midfile(synth.fixed64(30_000), at_record=12_345)
+    sm = check_parity(blob)
+    assert sm.n_records == 12_345
+
+
+def test_empty_and_header_only():
+    check_parity(synth.global_header())                           # 0 records, rem empty
+    check_parity(synth.global_header() + bytes(10))               # 0 records, 10-byte rem
+    check_parity(synth.global_header() + struct.pack("<IIII", 0, 0, 0, 0))  # one zero-length record
+
+
+def test_records_without_file_header():
+    """PcapRecords::parse(input, endianness) over bare records (start = 0)."""
+    body = synth.quirk_corpus(3_000, seed=4, with_header=False)
+    check_parity(body, start=0, endianness=npr.Endianness.Little)
+    body = synth.quirk_corpus(3_000, seed=4, with_header=False, big=True)
+    check_parity(body, start=0, endianness=npr.Endianness.Big)
+
+
+def test_workspace_reuse_many_launches():
+    blob = synth.quirk_corpus(5_000, seed=21, fake_every=9)
+    cap = len(blob) // 16 + 1
+    ws = device.Workspace(cap, cap, status=True)
+    for _ in range(5):
+        check_parity(blob, ws=ws)
+    check_parity(synth.fixed64(10_000), ws=ws)
+
+
+def test_flow_capacity_overflow_reports_exact_counts():
+    blob = synth.fixed64(5_000)
+    buf = to_dev(blob)
+    ws = device.Workspace(10_000, 100)
+    ws.launch(buf)
+    with pytest.raises(npr.DeviceError):
+        ws.check()
+    assert ws.last.n_flows == 5_000 and ws.last.n_records == 5_000 and ws.last.flags == 2
+
+
+def test_misaligned_input_rejected():
+    blob = synth.fixed64(100)
+    buf = to_dev(b"\0" + blob)
+    ws = device.Workspace(200, 200)
+    with pytest.raises(npr.DeviceError):
+        ws.launch(buf[1:])
+
+
+# ---- the dense extract / convert_records entry points over arbitrary record lists -----------
+def test_extract_flows_over_arbitrary_records():
+    blob = synth.quirk_corpus(4_000, seed=13)
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    recs = recs.copy()
+    rng = np.random.default_rng(0)
+    shrink = rng.random(len(recs)) < 0.2   # records whose payload is a prefix of the frame
+    recs["actual_length"][shrink] = (recs["actual_length"][shrink] * rng.random(shrink.sum())).astype(np.uint32)
+    perm = rng.permutation(len(recs))
+    recs = recs[perm]
+    want_f, want_v6, want_st = _oracle.extract_flows(blob, recs)
+    ctx = npr.context()
+    a = np.frombuffer(blob, dtype=np.uint8)
+    n = len(recs)
+    f = np.zeros(n, _abi.FLOW_DTYPE)
+    v6 = np.zeros(n, _abi.FLOW_V6_DTYPE)
+    st = np.zeros(n, np.uint8)
+    ctx.check(ctx.lib.npr_extract_flows(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, f.ctypes.data,
+                                        v6.ctypes.data, st.ctypes.data))
+    assert np.array_equal(st, want_st)
+    assert f.tobytes() == want_f.tobytes()
+    assert v6.tobytes() == want_v6.tobytes()
+    # convert_records over the same (permuted) list: reverse LIST order
+    wf, wv6 = _oracle.convert_records(blob, recs)
+    out = np.zeros(n, _abi.FLOW_DTYPE)
+    out6 = np.zeros(n, _abi.FLOW_V6_DTYPE)
+    import ctypes
+    k = ctypes.c_size_t(0)
+    ctx.check(ctx.lib.npr_convert_records(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, out.ctypes.data,
+                                          out6.ctypes.data, n, ctypes.byref(k)))
+    assert k.value == len(wf)
+    assert out[: k.value].tobytes() == wf.tobytes()
+    m = (wf["kind"] & _abi.KIND_IPV6) != 0
+    assert out6[: k.value][m].tobytes() == wv6[m].tobytes()
+
+
+def test_mirror_api_matches_oracle():
+    blob = synth.quirk_corpus(2_000, seed=17)
+    rem, f = npr.parse(blob)
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    assert len(rem) == len(blob) - cons and f.records.len() == len(recs)
+    pairs = npr.flow.convert_records(f.records.into_inner())
+    wf, _ = _oracle.convert_records(blob, recs)
+    assert [p[0].offset for p in pairs] == [int.from_bytes(bytes(x), "little") for x in wf["record_offset"]]
+    rem2, recs2 = npr.PcapRecords.parse(blob[24:], npr.Endianness.Little)
+    assert recs2.len() == len(recs)
+    recs_list = npr.CaptureParser.parse_file(blob)
+    assert len(recs_list) == len(recs)
