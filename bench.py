@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--copies", type=int, default=4)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,7 +80,8 @@ def main():
     hdr = npr.GlobalHeader.parse(blob[:24])[1]
     ws = device.Workspace(record_cap=n, flow_cap=n, device=local, records=False, offsets=False, status=False,
                           flows=True, flows_v6=True)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # an explicit stream: events bracket exactly our launches
+    torch.cuda.set_stream(stream)
 
     # correctness gate for the measured configuration
     ws.launch(bufs[0], start=24, endianness=hdr.endianness)
@@ -106,6 +108,28 @@ def main():
     sm = ws.check()
     assert sm.n_records == n and sm.n_flows == n
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    if args.stats:
+        import ctypes
+        lib, h = ws.ctx.lib, ws.ctx.handle
+        ws.ctx.check(lib.npr_ctx_set_stats(h, 2))
+        for i in range(3):
+            ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
+        ws.check()
+        st = (ctypes.c_uint32 * 8)()
+        ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
+        nt = (len(blob) + 16383) // 16384
+        stamps = np.zeros(nt * 8, dtype=np.uint64)
+        ntl = ctypes.c_uint64(0)
+        ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
+        sr = stamps.reshape(nt, 8)
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 8))
+        sr = stamps.reshape(nt, 8)
+        print(f"[rank {rank}] spins/tile={(sr[:, 7] & 0xfffff).mean():.2f} slides={(sr[:, 7] >> 20 & 0xfffff).sum()} "
+              f"mism_waits={(sr[:, 7] >> 40).sum()}", file=sys.stderr)
+        print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} spin={st[2]} slide={st[3]} "
+              f"weak={st[4]} none={st[5]} tiles={(len(blob) + 16383) // 16384}", file=sys.stderr, flush=True)
+        ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
 
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
     if world > 1:

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -29,6 +30,12 @@ struct npr_ctx {
   uint32_t *abort_word = nullptr;
   npr_summary *summary = nullptr;   // device
   npr_summary *summary_h = nullptr; // pinned host
+  uint32_t *stats = nullptr;        // device diagnostic counters (npr_ctx_set_stats)
+  int stats_mode = 0;               // 2 = also per-tile phase stamps
+  DevBuf stamps;
+  uint64_t stamp_tiles = 0;
+  int kernel = 1;          // 0 = one workgroup per tile, 1 = persistent pipelined (NPR_KERNEL=tile|pipe)
+  uint32_t pipe_grid = 0;  // resident workgroups of the pipelined kernel
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -104,9 +111,12 @@ extern "C" {
 const char *npr_version(void) { return NPR_VERSION_STRING; }
 int npr_abi_version(void) { return NPR_ABI_VERSION; }
 
-uint64_t npr_workspace_bytes(uint64_t len) {
-  return tiles_for(len, 0, nullptr) * sizeof(npr::TileSlot);
+// tile slots followed by group slots, one allocation (zeroed when (re)allocated)
+static uint64_t slot_bytes(uint64_t nt) {
+  return nt * sizeof(npr::TileSlot) + (nt / npr::kGroup + 1) * sizeof(npr::GroupSlot);
 }
+
+uint64_t npr_workspace_bytes(uint64_t len) { return slot_bytes(tiles_for(len, 0, nullptr)); }
 
 npr_status npr_ctx_create(int device, npr_ctx **out) {
   if (!out) return NPR_ERR_ARG;
@@ -122,6 +132,15 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
+  if (const char *k = getenv("NPR_KERNEL")) c->kernel = strcmp(k, "tile") == 0 ? 0 : 1;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    npr_ctx_destroy(c);
+    return NPR_ERR_DEVICE;
+  }
+  int per_cu = npr::pipe_blocks_per_cu();
+  if (const char *g = getenv("NPR_PIPE_PER_CU")) per_cu = atoi(g);
+  c->pipe_grid = (uint32_t)std::max(1, prop.multiProcessorCount * std::max(1, per_cu));
   *out = c;
   return NPR_OK;
 }
@@ -130,17 +149,56 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->slots, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+  for (DevBuf *b : {&c->slots, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->scratch})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
   if (c->summary) (void)hipFree(c->summary);
   if (c->summary_h) (void)hipHostFree(c->summary_h);
+  if (c->stats) (void)hipFree(c->stats);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
 const char *npr_ctx_last_error(const npr_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+npr_status npr_ctx_set_stats(npr_ctx *c, int enable) {
+  if (!c) return NPR_ERR_ARG;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  c->stats_mode = enable;
+  if (enable && !c->stats) {
+    HIP_CHECK(c, hipMalloc((void **)&c->stats, npr::kStatCount * sizeof(uint32_t)));
+    HIP_CHECK(c, hipMemset(c->stats, 0, npr::kStatCount * sizeof(uint32_t)));
+  } else if (!enable && c->stats) {
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    HIP_CHECK(c, hipFree(c->stats));
+    c->stats = nullptr;
+  }
+  return NPR_OK;
+}
+
+npr_status npr_ctx_read_stamps(npr_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_tiles) {
+  if (!c || !out) return NPR_ERR_ARG;
+  if (!c->stamps.p) return fail(c, NPR_ERR_ARG, "stamps not enabled (npr_ctx_set_stats(ctx, 2))");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  HIP_CHECK(c, hipDeviceSynchronize());
+  const uint64_t n = std::min<uint64_t>(cap, c->stamp_tiles * 8);
+  HIP_CHECK(c, hipMemcpy(out, c->stamps.p, n * 8, hipMemcpyDeviceToHost));
+  if (n_tiles) *n_tiles = c->stamp_tiles;
+  return NPR_OK;
+}
+
+npr_status npr_ctx_read_stats(npr_ctx *c, uint32_t *out, int n, int reset) {
+  if (!c || !out || n <= 0) return NPR_ERR_ARG;
+  if (!c->stats) return fail(c, NPR_ERR_ARG, "stats not enabled");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  HIP_CHECK(c, hipDeviceSynchronize());
+  uint32_t tmp[npr::kStatCount];
+  HIP_CHECK(c, hipMemcpy(tmp, c->stats, sizeof tmp, hipMemcpyDeviceToHost));
+  for (int i = 0; i < n && i < (int)npr::kStatCount; ++i) out[i] = tmp[i];
+  if (reset) HIP_CHECK(c, hipMemset(c->stats, 0, sizeof tmp));
+  return NPR_OK;
+}
 
 // ---- GlobalHeader::parse (src/global_header.rs:40-70) ----------------------------------------
 npr_status npr_global_header_parse(const uint8_t *in, size_t len, npr_global_header *out, size_t *consumed) {
@@ -188,7 +246,7 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   uint64_t org = 0;
   const uint64_t nt = tiles_for(len, start, &org);
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
-  npr_status st = ensure(c, c->slots, nt * sizeof(npr::TileSlot), true);
+  npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
   hipStream_t s = pick(c, stream);
   if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
@@ -205,9 +263,10 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   p.epoch = c->epoch;
   p.ntiles = (uint32_t)nt;
   p.frac_max = 1000000000u;
-  p.flags = 0;
+  p.flags = start >= 24 ? npr::kFlagMagicAtZero : 0u;  // bytes 0..3 hold the pcap magic
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
+  p.groups = (npr::GroupSlot *)((char *)c->slots.p + nt * sizeof(npr::TileSlot));
   p.abort_word = c->abort_word;
   p.rec_off = o->record_offsets;
   p.recs = o->records;
@@ -217,7 +276,19 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   p.flows_v6 = (uint32_t *)o->flows_v6;
   p.flow_cap = o->flow_cap;
   p.summary = o->summary;
-  HIP_CHECK(c, npr::launch_parse_extract(p, s));
+  p.stats = c->stats;
+  p.stamps = nullptr;
+  if (c->stats_mode >= 2) {
+    if ((st = ensure(c, c->stamps, nt * 64, true))) return st;
+    p.stamps = (uint64_t *)c->stamps.p;
+    c->stamp_tiles = nt;
+  }
+  if (c->kernel == 1) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->pipe_grid);
+    HIP_CHECK(c, npr::launch_parse_pipe(p, grid, s));
+  } else {
+    HIP_CHECK(c, npr::launch_parse_extract(p, s));
+  }
   return NPR_OK;
 }
 

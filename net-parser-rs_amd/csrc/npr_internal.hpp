@@ -24,8 +24,26 @@ struct alignas(64) TileSlot {
   uint64_t p[4];
 };
 
+// Two-level look-back: the last tile of every kGroup-tile group publishes a group aggregate.
+constexpr int kGroup = 64;
+struct alignas(32) GroupSlot {
+  uint64_t g[4];
+};
+
 enum : uint32_t {
-  kFlagSpecFirst = 1u,  // tile 0's entry is speculative too (shard that starts mid-stream)
+  kFlagSpecFirst = 1u,    // tile 0's entry is speculative too (shard that starts mid-stream)
+  kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
+};
+
+// optional diagnostic counters (ParseParams::stats, NULL in production launches)
+enum : uint32_t {
+  kStatRewalk = 0,     // tiles whose speculated entry was wrong (re-walked)
+  kStatMismWait = 1,   // look-back waits for a mismatching tile's exact prefix
+  kStatSpin = 2,       // look-back polls that found an unpublished predecessor
+  kStatSlide = 3,      // look-back windows with no exact prefix (slid 64 tiles further)
+  kStatWeakEntry = 4,  // tiles that used a weak speculation
+  kStatNoEntry = 5,    // tiles with no plausible record start
+  kStatCount = 8
 };
 
 struct ParseParams {
@@ -40,6 +58,7 @@ struct ParseParams {
   uint32_t flags;
   uint32_t timeout_ticks;  // s_memrealtime (100 MHz) ticks before a stalled hand-off aborts
   TileSlot *slots;
+  GroupSlot *groups;       // ntiles / kGroup
   uint32_t *abort_word;    // == epoch once any tile aborted
   uint64_t *rec_off;
   npr_record *recs;
@@ -49,9 +68,15 @@ struct ParseParams {
   uint32_t *flows_v6;      // npr_flow_v6 as 8 dwords
   uint64_t flow_cap;
   npr_summary *summary;
+  uint32_t *stats;         // kStatCount counters or NULL
+  uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][8] or NULL
+  uint64_t pcnt_slow;      // kernel-internal: record index base during a slow-path re-decode
 };
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
+// persistent pipelined variant: `grid` resident workgroups loop over the tiles
+hipError_t launch_parse_pipe(const ParseParams &p, uint32_t grid, hipStream_t s);
+int pipe_blocks_per_cu();
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);
