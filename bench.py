@@ -117,18 +117,14 @@ def main():
         ws.check()
         st = (ctypes.c_uint32 * 8)()
         ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
-        nt = (len(blob) + 16383) // 16384
-        stamps = np.zeros(nt * 8, dtype=np.uint64)
         ntl = ctypes.c_uint64(0)
+        ws.ctx.check(lib.npr_ctx_read_stamps(h, None, 0, ctypes.byref(ntl)))  # tile count of the last launch
+        nt = ntl.value
+        stamps = np.zeros(nt * 8, dtype=np.uint64)
         ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
-        sr = stamps.reshape(nt, 8)
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 8))
-        sr = stamps.reshape(nt, 8)
-        print(f"[rank {rank}] spins/tile={(sr[:, 7] & 0xfffff).mean():.2f} slides={(sr[:, 7] >> 20 & 0xfffff).sum()} "
-              f"mism_waits={(sr[:, 7] >> 40).sum()}", file=sys.stderr)
-        print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} spin={st[2]} slide={st[3]} "
-              f"weak={st[4]} none={st[5]} tiles={(len(blob) + 16383) // 16384}", file=sys.stderr, flush=True)
+        print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} tiles={nt}", file=sys.stderr, flush=True)
         ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
 
     t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)

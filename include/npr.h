@@ -174,14 +174,15 @@ npr_status npr_ctx_create(int device, npr_ctx **out);
 void npr_ctx_destroy(npr_ctx *ctx);
 const char *npr_ctx_last_error(const npr_ctx *ctx);
 /* Diagnostics: per-launch speculation / hand-off counters (off by default; costs atomics).
- * Counters: [0] tiles re-walked after a wrong speculation, [1] look-back waits on a mismatching
- * tile, [2] look-back polls of unpublished tiles, [3] look-back windows slid, [4] tiles that used
- * a weak speculation, [5] tiles with no plausible record start. */
+ * Counters: [0] tiles pass 2 re-walked (pass 1's entry was not the exact one), [1] prefix folds
+ * that waited for a mis-speculated tile's exact prefix, [5] tiles with no plausible record
+ * start; the others are reserved (0). */
 npr_status npr_ctx_set_stats(npr_ctx *ctx, int enable);
 npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
 /* With npr_ctx_set_stats(ctx, 2): per-tile s_memrealtime (100 MHz) stamps of the last parse,
- * 8 words per tile: [0] start [1] staged [2] speculated [3] walked+counted [4] prefix known
- * [5] done [6] (records << 32 | re-walked). */
+ * 8 words per tile: pass 1 [0] tile start [1] entry known [2] walked [3] counted [4] published;
+ * pass 2 [5] tile start [6] record offsets known [7] written.  out may be NULL with cap 0 to
+ * query *n_tiles only. */
 npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_tiles);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

@@ -34,8 +34,10 @@ struct npr_ctx {
   int stats_mode = 0;               // 2 = also per-tile phase stamps
   DevBuf stamps;
   uint64_t stamp_tiles = 0;
-  int kernel = 1;          // 0 = one workgroup per tile, 1 = persistent pipelined (NPR_KERNEL=tile|pipe)
-  uint32_t pipe_grid = 0;  // resident workgroups of the pipelined kernel
+  DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
+  DevBuf counters;         // arrival counters: cnt1[g] at word 2g, cnt2[h] at word 2h+1 (layout independent of the input)
+  bool dirty = false;
+  uint32_t grid_scan = 0, grid_emit = 0;  // persistent grids: CUs x resident workgroups per CU      // a launch timed out: counters may be non-zero -> clear before the next launch
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -111,12 +113,19 @@ extern "C" {
 const char *npr_version(void) { return NPR_VERSION_STRING; }
 int npr_abi_version(void) { return NPR_ABI_VERSION; }
 
-// tile slots followed by group slots, one allocation (zeroed when (re)allocated)
+static uint64_t ngroups1(uint64_t nt) { return (nt + npr::kGroup - 1) / npr::kGroup; }
+static uint64_t ngroups2(uint64_t nt) { return (ngroups1(nt) + npr::kGroup - 1) / npr::kGroup; }
+// tile slots, then G1 slots, then G2 slots: one allocation (granules are epoch-tagged, so the
+// layout may shift between launches)
 static uint64_t slot_bytes(uint64_t nt) {
-  return nt * sizeof(npr::TileSlot) + (nt / npr::kGroup + 1) * sizeof(npr::GroupSlot);
+  return nt * sizeof(npr::TileSlot) + (ngroups1(nt) + ngroups2(nt)) * sizeof(npr::GroupSlot);
 }
+static uint64_t counter_bytes(uint64_t nt) { return (2 * ngroups1(nt) + 2) * sizeof(uint32_t); }
 
-uint64_t npr_workspace_bytes(uint64_t len) { return slot_bytes(tiles_for(len, 0, nullptr)); }
+uint64_t npr_workspace_bytes(uint64_t len) {
+  const uint64_t nt = tiles_for(len, 0, nullptr);
+  return slot_bytes(nt) + counter_bytes(nt) + nt * npr::kMaxRec * sizeof(uint16_t);
+}
 
 npr_status npr_ctx_create(int device, npr_ctx **out) {
   if (!out) return NPR_ERR_ARG;
@@ -132,15 +141,20 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
-  if (const char *k = getenv("NPR_KERNEL")) c->kernel = strcmp(k, "tile") == 0 ? 0 : 1;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
-  int per_cu = npr::pipe_blocks_per_cu();
-  if (const char *g = getenv("NPR_PIPE_PER_CU")) per_cu = atoi(g);
-  c->pipe_grid = (uint32_t)std::max(1, prop.multiProcessorCount * std::max(1, per_cu));
+  // NPR_FUSED=0 selects the two-launch variant (per-pass profiling); NPR_*_PER_CU override occupancy
+  const char *fz = getenv("NPR_FUSED");
+  const bool fused = !(fz && strcmp(fz, "0") == 0);
+  int per_cu_scan = fused ? npr::fused_blocks_per_cu() : npr::scan_blocks_per_cu();
+  int per_cu_emit = fused ? 0 : npr::emit_blocks_per_cu();
+  if (const char *v = getenv("NPR_SCAN_PER_CU")) per_cu_scan = std::max(1, atoi(v));
+  if (const char *v = getenv("NPR_EMIT_PER_CU"); v && !fused) per_cu_emit = std::max(1, atoi(v));
+  c->grid_scan = (uint32_t)(prop.multiProcessorCount * per_cu_scan);
+  c->grid_emit = (uint32_t)(prop.multiProcessorCount * per_cu_emit);
   *out = c;
   return NPR_OK;
 }
@@ -149,7 +163,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->slots, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+  for (DevBuf *b : {&c->slots, &c->srec, &c->counters, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->scratch})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
@@ -178,12 +192,12 @@ npr_status npr_ctx_set_stats(npr_ctx *c, int enable) {
 }
 
 npr_status npr_ctx_read_stamps(npr_ctx *c, uint64_t *out, uint64_t cap, uint64_t *n_tiles) {
-  if (!c || !out) return NPR_ERR_ARG;
+  if (!c || (!out && cap)) return NPR_ERR_ARG;
   if (!c->stamps.p) return fail(c, NPR_ERR_ARG, "stamps not enabled (npr_ctx_set_stats(ctx, 2))");
   HIP_CHECK(c, hipSetDevice(c->device));
   HIP_CHECK(c, hipDeviceSynchronize());
   const uint64_t n = std::min<uint64_t>(cap, c->stamp_tiles * 8);
-  HIP_CHECK(c, hipMemcpy(out, c->stamps.p, n * 8, hipMemcpyDeviceToHost));
+  if (n) HIP_CHECK(c, hipMemcpy(out, c->stamps.p, n * 8, hipMemcpyDeviceToHost));
   if (n_tiles) *n_tiles = c->stamp_tiles;
   return NPR_OK;
 }
@@ -248,11 +262,17 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
+  if ((st = ensure(c, c->counters, counter_bytes(nt), true))) return st;
+  if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
   hipStream_t s = pick(c, stream);
   if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
     c->epoch = 1;
     HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
     HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, 64, s));
+  }
+  if (c->dirty) {  // the previous launch aborted part-way: arrival counters are stale
+    HIP_CHECK(c, hipMemsetAsync(c->counters.p, 0, c->counters.cap, s));
+    c->dirty = false;
   }
   npr::ParseParams p{};
   p.buf = (const uint8_t *)input;
@@ -266,7 +286,13 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   p.flags = start >= 24 ? npr::kFlagMagicAtZero : 0u;  // bytes 0..3 hold the pcap magic
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
-  p.groups = (npr::GroupSlot *)((char *)c->slots.p + nt * sizeof(npr::TileSlot));
+  p.ngroups1 = (uint32_t)ngroups1(nt);
+  p.ngroups2 = (uint32_t)ngroups2(nt);
+  p.groups1 = (npr::GroupSlot *)((char *)c->slots.p + nt * sizeof(npr::TileSlot));
+  p.groups2 = p.groups1 + p.ngroups1;
+  p.cnt1 = (uint32_t *)c->counters.p;      // word 2g
+  p.cnt2 = (uint32_t *)c->counters.p + 1;  // word 2h + 1
+  p.srec_g = (uint16_t *)c->srec.p;
   p.abort_word = c->abort_word;
   p.rec_off = o->record_offsets;
   p.recs = o->records;
@@ -283,12 +309,7 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
     p.stamps = (uint64_t *)c->stamps.p;
     c->stamp_tiles = nt;
   }
-  if (c->kernel == 1) {
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(nt, c->pipe_grid);
-    HIP_CHECK(c, npr::launch_parse_pipe(p, grid, s));
-  } else {
-    HIP_CHECK(c, npr::launch_parse_extract(p, s));
-  }
+  HIP_CHECK(c, npr::launch_parse_extract(p, c->grid_scan, c->grid_emit, s));
   return NPR_OK;
 }
 
@@ -298,8 +319,10 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   HIP_CHECK(c, hipMemcpyAsync(c->summary_h, o->summary, sizeof(npr_summary), hipMemcpyDeviceToHost, s));
   HIP_CHECK(c, hipStreamSynchronize(s));
   if (hs) *hs = *c->summary_h;
-  if (c->summary_h->epoch != c->epoch)
+  if (c->summary_h->epoch != c->epoch) {
+    c->dirty = true;
     return fail(c, NPR_ERR_TIMEOUT, "parse did not complete (tile hand-off timed out)");
+  }
   if (c->summary_h->flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded (flags=%u)", c->summary_h->flags);
   return NPR_OK;
 }

@@ -9,38 +9,37 @@
 
 namespace npr {
 
-// Tile geometry of the fused parse+extract kernel.
-constexpr int kBlock = 256;            // 4 waves
-constexpr int kTile = 16384;           // bytes of the record stream owned by one workgroup
-constexpr int kHalo = 256;             // bytes staged past the tile (headers of straddling records)
-constexpr int kStage = kTile + kHalo;  // bytes staged in LDS per workgroup
+// Tile geometry of the parse+extract kernels: ONE WAVE per tile.
+constexpr int kBlock = 256;            // workgroup size of the auxiliary kernels (dense extract, compaction)
+constexpr int kWave = 64;              // the parse kernels: one-wave workgroups
+constexpr int kTile = 4096;            // bytes of the record stream owned by one tile
+constexpr int kHalo = 128;             // bytes staged past the tile (headers + fast-decode window of straddlers)
+constexpr int kStage = kTile + kHalo;  // bytes staged in LDS per tile
 constexpr int kMaxRec = kTile / 16;    // every record is >= 16 B
-constexpr int kSlots = kMaxRec / kBlock;
+constexpr int kRounds = kMaxRec / kWave;  // decode rounds of 64 records
 
-// Per-tile hand-off slot: A = speculative aggregate, P = exact inclusive prefix.  Each word is
-// an 8-byte {tag:16 | value:48} granule written by ONE agent-scope store (self-validating).
+// Per-tile hand-off slot: A = speculative aggregate (k_scan_tiles), P = exact inclusive prefix
+// (k_emit_tiles).  Each word is an 8-byte {tag:16 | value:48} granule written by ONE
+// agent-scope store (self-validating: tag = the launch epoch).
 struct alignas(64) TileSlot {
   uint64_t a[4];
   uint64_t p[4];
 };
 
-// Two-level look-back: the last tile of every kGroup-tile group publishes a group aggregate.
+// Aggregates of 64 tiles (G1) and of 64 G1s = 4096 tiles (G2), folded by the last arriver.
 constexpr int kGroup = 64;
 struct alignas(32) GroupSlot {
   uint64_t g[4];
 };
 
 enum : uint32_t {
-  kFlagSpecFirst = 1u,    // tile 0's entry is speculative too (shard that starts mid-stream)
   kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
 };
 
 // optional diagnostic counters (ParseParams::stats, NULL in production launches)
 enum : uint32_t {
-  kStatRewalk = 0,     // tiles whose speculated entry was wrong (re-walked)
-  kStatMismWait = 1,   // look-back waits for a mismatching tile's exact prefix
-  kStatSpin = 2,       // look-back polls that found an unpublished predecessor
-  kStatSlide = 3,      // look-back windows with no exact prefix (slid 64 tiles further)
+  kStatRewalk = 0,     // tiles pass 2 re-walked (pass 1's entry was not the exact one)
+  kStatMismWait = 1,   // prefix folds that waited for a mis-speculated tile's exact prefix
   kStatWeakEntry = 4,  // tiles that used a weak speculation
   kStatNoEntry = 5,    // tiles with no plausible record start
   kStatCount = 8
@@ -58,7 +57,11 @@ struct ParseParams {
   uint32_t flags;
   uint32_t timeout_ticks;  // s_memrealtime (100 MHz) ticks before a stalled hand-off aborts
   TileSlot *slots;
-  GroupSlot *groups;       // ntiles / kGroup
+  GroupSlot *groups1;      // ngroups1 = ceil(ntiles / 64)
+  GroupSlot *groups2;      // ceil(ngroups1 / 64)
+  uint32_t *cnt1, *cnt2;   // arrival counters (zero between launches)
+  uint32_t ngroups1, ngroups2;
+  uint16_t *srec_g;        // pass-1 record offsets, kMaxRec per tile (pass 2 reuses them)
   uint32_t *abort_word;    // == epoch once any tile aborted
   uint64_t *rec_off;
   npr_record *recs;
@@ -70,13 +73,15 @@ struct ParseParams {
   npr_summary *summary;
   uint32_t *stats;         // kStatCount counters or NULL
   uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][8] or NULL
-  uint64_t pcnt_slow;      // kernel-internal: record index base during a slow-path re-decode
 };
 
-hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
-// persistent pipelined variant: `grid` resident workgroups loop over the tiles
-hipError_t launch_parse_pipe(const ParseParams &p, uint32_t grid, hipStream_t s);
-int pipe_blocks_per_cu();
+// Persistent grids (capped at ntiles) whose workgroups each own a contiguous run of tiles:
+// grid_emit == 0 -> one fused launch (k_parse_fused, grid_scan workgroups); else k_scan_tiles
+// then k_emit_tiles.
+hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s);
+int scan_blocks_per_cu();  // resident workgroups per CU (occupancy API)
+int emit_blocks_per_cu();
+int fused_blocks_per_cu();
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);

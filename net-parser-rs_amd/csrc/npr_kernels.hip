@@ -255,752 +255,11 @@ __device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f)
 }
 
 // ---------------------------------------------------------------------------------------------
-// tile hand-off granules (MI355X_MICROARCH.md "R2": the data IS the flag, {tag, value} 8-B)
+// fast decode: Ethernet (untagged) / IPv4 (IHL 5) or IPv6 (no extension) / TCP or UDP.
+// Branch-light: 17 aligned LDS words + v_alignbyte, static field offsets, status by selects;
+// bit-identical to decode<> for these shapes.  Returns 0xff for any other frame (the caller then
+// runs the general decode<>).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t gran(uint32_t tag, uint64_t v) { return ((uint64_t)tag << 48) | (v & kMask48); }
-__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
-  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
-  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// A segment of consecutive tiles [first, last] under speculation.
-struct Seg {
-  uint64_t entry, exit, cnt, ok;
-  int64_t first, last, mism;  // mism: lowest tile whose speculated entry is contradicted
-  bool valid;
-};
-
-__device__ __forceinline__ uint64_t tile_end(const ParseParams &kp, int64_t k) {
-  const uint64_t e = kp.org + (uint64_t)(k + 1) * kTile;
-  return e < kp.len ? e : kp.len;
-}
-
-// Chain-consistency monoid: X then Y (Y starts right after X).
-__device__ __forceinline__ Seg combine(const ParseParams &kp, const Seg &X, const Seg &Y) {
-  Seg r = X;
-  r.last = Y.last;
-  if (!X.valid) return r;                                 // keep the lowest mismatch
-  if (X.exit < tile_end(kp, X.last)) return r;            // chain ended inside X: Y is moot
-  if (X.exit != Y.entry) {                                // Y's speculated start is wrong
-    r.valid = false;
-    r.mism = Y.first;
-    return r;
-  }
-  r.exit = Y.exit;
-  r.cnt = X.cnt + Y.cnt;
-  r.ok = X.ok + Y.ok;
-  r.valid = Y.valid;
-  r.mism = Y.mism;
-  return r;
-}
-
-// Bounded wait: false once the grid aborted or this wait exceeded the time budget.
-__device__ __forceinline__ bool spin_ok(const ParseParams &kp, uint64_t t0) {
-  __builtin_amdgcn_s_sleep(1);
-  if (__hip_atomic_load(kp.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kp.epoch) return false;
-  if (__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
-    __hip_atomic_store(kp.abort_word, kp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return false;
-  }
-  return true;
-}
-
-struct Prefix {
-  uint64_t exit, cnt, ok;
-};
-
-// diagnostic counters of the current wave (kept in registers; written to the stamp row)
-struct Diag {
-  uint32_t spins = 0, slides = 0, mism = 0;
-};
-
-// One lane's view of one segment of the look-back window: a tile, or a group of kGroup tiles.
-struct LaneSeg {
-  uint64_t entry, exit, cnt, ok;
-  int64_t first, last, mism;
-  bool present;  // an aggregate or an exact prefix has been published
-  bool anchor;   // exact inclusive prefix through `last` (cnt/ok are absolute)
-  bool valid;
-};
-
-__device__ __forceinline__ bool tagged(uint64_t w, uint32_t ep) { return (w >> 48) == ep; }
-
-// tile k: P (exact prefix) or A (speculative aggregate); all six granules are loaded at once
-__device__ __forceinline__ LaneSeg load_tile(const ParseParams &kp, int64_t k, bool inr) {
-  LaneSeg L{};
-  L.first = L.last = k;
-  L.mism = -1;
-  L.valid = true;
-  if (!inr) return L;
-  const uint32_t ep = kp.epoch;
-  const TileSlot *s = kp.slots + k;
-  const uint64_t p0 = ld_agent(&s->p[0]), p1 = ld_agent(&s->p[1]), p2 = ld_agent(&s->p[2]);
-  const uint64_t a0 = ld_agent(&s->a[0]), a1 = ld_agent(&s->a[1]), a2 = ld_agent(&s->a[2]);
-  if (tagged(p0, ep) && tagged(p1, ep) && tagged(p2, ep)) {
-    L.present = L.anchor = true;
-    L.exit = p0 & kMask48;
-    L.cnt = p1 & kMask48;
-    L.ok = p2 & kMask48;
-  } else if (tagged(a0, ep) && tagged(a1, ep) && tagged(a2, ep)) {
-    L.present = true;
-    const uint64_t e1 = a1 & kMask48, c = a2 & kMask48;
-    L.entry = e1 ? e1 - 1 : kNone;
-    L.exit = a0 & kMask48;
-    L.cnt = c & 0xffffffull;
-    L.ok = (c >> 24) & 0xffffffull;
-  }
-  return L;
-}
-
-// group gg (tiles [gg*kGroup, gg*kGroup + kGroup)): the exact prefix of its last tile, or the
-// group aggregate G published by that tile (anchored when it was folded from an exact prefix)
-__device__ __forceinline__ LaneSeg load_group(const ParseParams &kp, int64_t gg, bool inr) {
-  LaneSeg L{};
-  L.first = gg * kGroup;
-  L.last = gg * kGroup + kGroup - 1;
-  L.mism = -1;
-  L.valid = true;
-  if (!inr) return L;
-  const uint32_t ep = kp.epoch;
-  const TileSlot *s = kp.slots + L.last;
-  const GroupSlot *g = kp.groups + gg;
-  const uint64_t p0 = ld_agent(&s->p[0]), p1 = ld_agent(&s->p[1]), p2 = ld_agent(&s->p[2]);
-  const uint64_t g0 = ld_agent(&g->g[0]), g1 = ld_agent(&g->g[1]), g2 = ld_agent(&g->g[2]),
-                 g3 = ld_agent(&g->g[3]);
-  if (tagged(p0, ep) && tagged(p1, ep) && tagged(p2, ep)) {
-    L.present = L.anchor = true;
-    L.exit = p0 & kMask48;
-    L.cnt = p1 & kMask48;
-    L.ok = p2 & kMask48;
-  } else if (tagged(g0, ep) && tagged(g1, ep) && tagged(g2, ep) && tagged(g3, ep)) {
-    L.present = true;
-    const uint64_t e1 = g1 & kMask48, w3 = g3 & kMask48;
-    L.entry = e1 ? e1 - 1 : kNone;
-    L.exit = g0 & kMask48;
-    L.cnt = g2 & kMask48;
-    L.ok = w3 & ((1ull << 40) - 1);
-    L.valid = (w3 >> 40) & 1ull;
-    L.anchor = (w3 >> 41) & 1ull;
-    L.mism = L.valid ? -1 : L.first + (int64_t)((w3 >> 42) & 63ull);
-  }
-  return L;
-}
-
-__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1);
-  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
-    v += ((uint64_t)hi << 32) | lo;
-  }
-  return v;
-}
-
-// Fold the window lanes [lo .. 0] (ascending tile order = descending lane) into one segment.
-// Every lane <= lo must be present.  Fast path: all links consistent, no END, all valid ->
-// two wave sums; otherwise the serial monoid (wave-uniform, readlane).
-__device__ Seg fold_window(const ParseParams &kp, const LaneSeg &L, int lo) {
-  const int lane = (int)(threadIdx.x & 63u);
-  const uint64_t prev_exit = shfl_down64(L.exit);  // exit of the preceding segment (lane + 1)
-  const bool inr = lane <= lo;
-  const bool bad = lane < lo && (!L.valid || L.entry != prev_exit);
-  const bool endc = inr && L.exit < tile_end(kp, L.last);
-  const bool lo_bad = lane == lo && !L.valid;
-  Seg r;
-  if (__ballot(bad || endc || lo_bad) == 0ull) {
-    r.cnt = wave_sum64(inr ? L.cnt : 0ull);
-    r.ok = wave_sum64(inr ? L.ok : 0ull);
-    r.entry = rl64(L.entry, lo);
-    r.exit = rl64(L.exit, 0);
-    r.first = (int64_t)rl64((uint64_t)L.first, lo);
-    r.last = (int64_t)rl64((uint64_t)L.last, 0);
-    r.mism = -1;
-    r.valid = true;
-    return r;
-  }
-  auto lane_seg = [&](int j) {
-    Seg y;
-    y.entry = rl64(L.entry, j);
-    y.exit = rl64(L.exit, j);
-    y.cnt = rl64(L.cnt, j);
-    y.ok = rl64(L.ok, j);
-    y.first = (int64_t)rl64((uint64_t)L.first, j);
-    y.last = (int64_t)rl64((uint64_t)L.last, j);
-    y.mism = (int64_t)rl64((uint64_t)L.mism, j);
-    y.valid = (__ballot(L.valid) >> j) & 1ull;
-    return y;
-  };
-  r = lane_seg(lo);
-  for (int j = lo - 1; j >= 0; --j) r = combine(kp, r, lane_seg(j));
-  return r;
-}
-
-// Wait for the exact prefix that resolves mismatching tile m: its own P when m is in tile t's
-// group (the tile-level window will see it), else the P of the last tile of m's group.
-__device__ bool wait_resolved(const ParseParams &kp, int64_t m, uint32_t g, uint64_t t0, Diag &dg) {
-  dg.mism += 1;
-  const int64_t gm = m / kGroup;
-  const int64_t k = gm == (int64_t)g ? m : gm * kGroup + kGroup - 1;
-  const TileSlot *s = kp.slots + k;
-  for (;;) {
-    const uint64_t p0 = ld_agent(&s->p[0]), p1 = ld_agent(&s->p[1]), p2 = ld_agent(&s->p[2]);
-    const bool ok = tagged(p0, kp.epoch) && tagged(p1, kp.epoch) && tagged(p2, kp.epoch);
-    if (__ballot(ok) & 1ull) return true;
-    if (!spin_ok(kp, t0)) return false;
-  }
-}
-
-// Two-level decoupled look-back for tile t (wave 0; every lane returns the same result).
-//   L1: the tiles of t's own group before t — an exact prefix there ends the search;
-//   L2: the groups before — exact group prefixes (P of a group's last tile) or group aggregates,
-//       64 groups (4096 tiles) per poll, sliding further back only if no exact prefix is in range.
-// Any inconsistency is resolved by waiting for the exact prefix of the offending tile/group.
-__device__ bool lookback(const ParseParams &kp, uint32_t t, Prefix &out, Diag &dg) {
-  const int lane = (int)(threadIdx.x & 63u);
-  const uint32_t g = t / kGroup, i = t % kGroup;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {  // restart point after waiting for a mismatch to resolve
-    bool restart = false;
-    Seg S{};
-    bool s_has = false;
-    if (i > 0) {  // ---- L1
-      for (;;) {
-        const bool inr = lane < (int)i;
-        const LaneSeg L = load_tile(kp, (int64_t)t - 1 - lane, inr);
-        const uint64_t bAnc = __ballot(inr && L.anchor), bPres = __ballot(inr && L.present);
-        const int jp = bAnc ? __builtin_ctzll(bAnc) : (int)i;
-        const uint64_t need = jp >= 64 ? ~0ull : ((1ull << jp) - 1ull);
-        const uint64_t need_in = jp < (int)i ? need : (i >= 64 ? ~0ull : ((1ull << i) - 1ull));
-        if ((bPres & need_in) != need_in) {
-          ++dg.spins;
-          if (!spin_ok(kp, t0)) return false;
-          continue;
-        }
-        const Seg cur = fold_window(kp, L, jp < (int)i ? jp : (int)i - 1);
-        if (jp < (int)i) {
-          if (cur.valid) {
-            out.exit = cur.exit;
-            out.cnt = cur.cnt;
-            out.ok = cur.ok;
-            return true;
-          }
-          if (!wait_resolved(kp, cur.mism, g, t0, dg)) return false;
-          restart = true;
-        } else {
-          S = cur;
-          s_has = true;
-        }
-        break;
-      }
-      if (restart) continue;
-    }
-    // ---- L2 (g >= 1 here: in group 0 tile 0's exact prefix is always inside the L1 window)
-    int64_t gh = (int64_t)g - 1;
-    for (;;) {
-      const int64_t gg = gh - lane;
-      const bool inr = gg >= 0;
-      const LaneSeg L = load_group(kp, gg, inr);
-      const int n = gh + 1 < 64 ? (int)(gh + 1) : 64;
-      const uint64_t bAnc = __ballot(inr && L.anchor), bPres = __ballot(inr && L.present);
-      const int jp = bAnc ? __builtin_ctzll(bAnc) : n;
-      const uint64_t need = jp >= 64 ? ~0ull : ((1ull << jp) - 1ull);
-      if ((bPres & need) != need) {
-        ++dg.spins;
-        if (!spin_ok(kp, t0)) return false;
-        continue;
-      }
-      Seg cur = fold_window(kp, L, jp < n ? jp : n - 1);
-      if (s_has) cur = combine(kp, cur, S);
-      if (jp < n) {
-        if (cur.valid) {
-          out.exit = cur.exit;
-          out.cnt = cur.cnt;
-          out.ok = cur.ok;
-          return true;
-        }
-        if (!wait_resolved(kp, cur.mism, g, t0, dg)) return false;
-        restart = true;
-        break;
-      }
-      dg.slides += 1;
-      S = cur;
-      s_has = true;
-      gh -= 64;
-    }
-    (void)restart;
-  }
-}
-
-// Tile gL*kGroup + kGroup-1 (wave 0), right after publishing its own aggregate: fold the group's
-// 64 tile records into one group aggregate G (anchored when an exact prefix is among them).
-__device__ bool publish_group(const ParseParams &kp, uint32_t gL) {
-  const int lane = (int)(threadIdx.x & 63u);
-  const uint32_t ep = kp.epoch;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  const int64_t last = (int64_t)gL * kGroup + kGroup - 1;
-  for (;;) {
-    const LaneSeg L = load_tile(kp, last - lane, true);
-    const uint64_t bAnc = __ballot(L.anchor), bPres = __ballot(L.present);
-    const int jp = bAnc ? __builtin_ctzll(bAnc) : 64;
-    const uint64_t need = jp >= 64 ? ~0ull : ((1ull << jp) - 1ull);
-    if ((bPres & need) != need) {
-      if (!spin_ok(kp, t0)) return false;
-      continue;
-    }
-    const Seg cur = fold_window(kp, L, jp < 64 ? jp : 63);
-    if (lane == 0) {
-      GroupSlot *G = kp.groups + gL;
-      const bool anchored = jp < 64;
-      const uint64_t mrel = cur.valid ? 0ull : (uint64_t)(cur.mism - (int64_t)gL * kGroup) & 63ull;
-      st_agent(&G->g[0], gran(ep, cur.exit));
-      st_agent(&G->g[1], gran(ep, (anchored || cur.entry == kNone) ? 0ull : cur.entry + 1));
-      st_agent(&G->g[2], gran(ep, cur.cnt));
-      st_agent(&G->g[3], gran(ep, (cur.ok & ((1ull << 40) - 1)) | ((uint64_t)cur.valid << 40) |
-                                      ((uint64_t)anchored << 41) | (mrel << 42)));
-    }
-    return true;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// speculation + chain walk
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool plaus1(uint32_t frac, uint32_t incl, uint32_t orig, uint32_t frac_max) {
-  return incl >= 1u && incl <= kInclMax && orig >= incl && frac < frac_max;
-}
-
-// How plausible is LDS offset rel (absolute p) as a record start?  0 = no; 1 = weak (its header
-// passes but fewer than two chained headers could be checked inside the staged window);
-// 2 = strong (two further headers check out, or the chain ends exactly at EOF).  A heuristic
-// only: the look-back verifies every guess, a wrong one costs a re-walk, never a wrong result.
-__device__ int plausibility(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t rel,
-                            uint32_t frac_max) {
-  const bool big = kp.big;
-  const uint64_t p = tile_lo + rel;
-  if (kp.len - p < 16) return 0;
-  uint32_t ts = hdr(w, rel, 0, big);
-  const uint32_t incl = hdr(w, rel, 2, big);
-  if (!plaus1(hdr(w, rel, 1, big), incl, hdr(w, rel, 3, big), frac_max)) return 0;
-  if (kp.len - p - 16 < incl) return 0;
-  uint64_t q = p + 16 + incl;
-  int verified = 0;
-  for (int hop = 0; hop < 3; ++hop) {
-    if (q == kp.len) return 2;                                // chain ends exactly at EOF
-    const uint64_t qr = q - tile_lo;
-    if (qr + 16 > (uint64_t)kStage) return verified >= 2 ? 2 : 1;  // beyond the window
-    if (kp.len - q < 16) return verified >= 1 ? 2 : 1;         // truncated tail
-    const uint32_t r = (uint32_t)qr;
-    const uint32_t ts2 = hdr(w, r, 0, big), incl2 = hdr(w, r, 2, big);
-    if (!plaus1(hdr(w, r, 1, big), incl2, hdr(w, r, 3, big), frac_max)) return 0;
-    if (ts2 - ts + kTsWindow > 2u * kTsWindow) return 0;
-    ++verified;
-    if (kp.len - q - 16 < incl2) return verified >= 2 ? 2 : 1;  // truncated final record
-    ts = ts2;
-    q = q + 16 + incl2;
-  }
-  return 2;
-}
-
-// PcapRecords::parse loop (src/record.rs:30-49) over one tile, from `entry`, by wave 0.
-// Records whose header starts before tile_hi belong to this tile.  Returns the exit: the first
-// chain offset >= tile_hi, or (chain END, Q3) the offset of the first incomplete record.
-__device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec,
-                              uint64_t tile_lo, uint64_t tile_hi, uint64_t entry, uint32_t &n_out) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const bool big = kp.big;
-  uint64_t p = entry;
-  uint32_t n = 0;
-  while (p < tile_hi) {
-    const uint32_t incl = hdr(w, (uint32_t)(p - tile_lo), 2, big);
-    if (kp.len - p < 16 || kp.len - p - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
-    const uint64_t stride = 16ull + incl;
-    // stride speculation: lane j confirms the record at p + j*stride has the same length
-    const uint64_t q = p + (uint64_t)lane * stride;
-    bool ok = lane == 0;
-    if (lane != 0 && q < tile_hi)
-      ok = hdr(w, (uint32_t)(q - tile_lo), 2, big) == incl && kp.len - q >= stride;
-    const uint64_t b = __ballot(ok);
-    const uint32_t m = (~b == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~b);
-    if (lane < m) srec[n + lane] = (uint16_t)(q - tile_lo);
-    n += m;
-    p += (uint64_t)m * stride;
-  }
-  n_out = n;
-  return p;
-}
-
-// Decode every record of the tile (status only) and count Ok flows per (slot, wave).
-__device__ uint32_t count_pass(const ParseParams &kp, const uint32_t *w, const uint16_t *srec,
-                               uint32_t n, uint64_t tile_lo, uint32_t (*scnt)[4]) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint8_t *b = (const uint8_t *)w;
-#pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
-    const uint32_t i = tid + (uint32_t)s * kBlock;
-    bool ok = false;
-    if (i < n) {
-      const uint32_t rel = srec[i];
-      const uint64_t p = tile_lo + rel;
-      const uint32_t incl = hdr(w, rel, 2, kp.big);
-      TileReader r{w, b, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
-      FlowWords f;
-      ok = decode<false>(r, incl, f) == NPR_FLOW_OK;
-    }
-    const uint64_t bal = __ballot(ok);
-    if (lane == 0) scnt[s][wave] = (uint32_t)__builtin_popcountll(bal);
-  }
-  __syncthreads();
-  uint32_t tot = 0;
-#pragma unroll
-  for (int s = 0; s < kSlots; ++s) tot += scnt[s][0] + scnt[s][1] + scnt[s][2] + scnt[s][3];
-  return tot;
-}
-
-__device__ __forceinline__ void stamp(const ParseParams &kp, uint32_t t, int k) {
-  if (kp.stamps && threadIdx.x == 0) kp.stamps[(uint64_t)t * 8 + k] = __builtin_amdgcn_s_memrealtime();
-}
-
-// ---------------------------------------------------------------------------------------------
-// the fused kernel
-// ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_parse_extract(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) uint32_t sw[kStage / 4 + 4];
-  __shared__ uint16_t srec[kMaxRec];
-  __shared__ uint32_t scnt[kSlots][4];
-  __shared__ uint32_t s_cand, s_weak, s_n, s_abort;
-  __shared__ uint64_t s_entry, s_exit, s_pexit, s_pcnt, s_pok;
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t t = blockIdx.x;
-  const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-  const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
-  const bool big = kp.big;
-  stamp(kp, t, 0);
-
-  // 1. stage [tile_lo, tile_lo + kStage) into LDS.  The descriptor range is rounded up to the
-  //    16-B chunk so a partially valid last chunk is read whole (same page); bytes past it read 0.
-  {
-    const uint64_t avail = kp.len > tile_lo ? kp.len - tile_lo : 0;
-    uint32_t nbytes = avail < (uint64_t)kStage ? (uint32_t)avail : (uint32_t)kStage;
-    nbytes = (nbytes + 15u) & ~15u;
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + tile_lo), 0, (int)nbytes, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < (kStage / 16 + kBlock - 1) / kBlock; ++i) {
-      const uint32_t c = tid + (uint32_t)i * kBlock;
-      if (c < kStage / 16) {
-        auto v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(c * 16u), 0, 0);
-        *reinterpret_cast<decltype(v) *>(&sw[c * 4]) = v;
-      }
-    }
-    if (tid < 4) sw[kStage / 4 + tid] = 0;
-  }
-  __syncthreads();
-  stamp(kp, t, 1);
-
-  // 2. entry: exact for tile 0, speculated otherwise (first strong candidate, else first weak)
-  uint64_t entry;
-  if (t == 0 && !(kp.flags & kFlagSpecFirst)) {
-    entry = kp.start;
-  } else {
-    uint32_t frac_max = kp.frac_max;
-    if (kp.flags & kFlagMagicAtZero) {  // pcap magic: microsecond captures bound ts_usec < 1e6
-      const uint32_t m = *reinterpret_cast<const uint32_t *>(kp.buf);
-      if (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u) frac_max = 1000000u;
-    }
-    if (tid == 0) {
-      s_cand = 0xffffffffu;
-      s_weak = 0xffffffffu;
-    }
-    __syncthreads();
-    const uint64_t lo = (t == 0) ? kp.start : tile_lo;
-    const uint32_t span = (uint32_t)(tile_hi - tile_lo);
-    for (uint32_t base = (uint32_t)(lo - tile_lo); base < span; base += kBlock) {
-      const uint32_t rel = base + tid;
-      const int grade = rel < span ? plausibility(kp, sw, tile_lo, rel, frac_max) : 0;
-      if (grade == 2) atomicMin(&s_cand, rel);
-      else if (grade == 1) atomicMin(&s_weak, rel);
-      if (__syncthreads_or(grade == 2)) break;
-    }
-    const uint32_t c = s_cand != 0xffffffffu ? s_cand : s_weak;
-    entry = c == 0xffffffffu ? kNone : tile_lo + c;
-    if (kp.stats && tid == 0) {
-      if (s_cand == 0xffffffffu) atomicAdd(&kp.stats[c == 0xffffffffu ? kStatNoEntry : kStatWeakEntry], 1u);  // rare
-    }
-  }
-
-  stamp(kp, t, 2);
-  // 3. speculative walk (wave 0)
-  if (wave == 0) {
-    uint32_t n = 0;
-    uint64_t ex = 0;
-    if (entry != kNone) ex = walk_tile(kp, sw, srec, tile_lo, tile_hi, entry, n);
-    if (lane == 0) {
-      s_n = n;
-      s_entry = entry;
-      s_exit = ex;
-    }
-  }
-  __syncthreads();
-
-  // 4. Ok-flow count of the speculative record set
-  uint32_t okc = count_pass(kp, sw, srec, s_n, tile_lo, scnt);
-  stamp(kp, t, 3);
-
-  // 5. publish, 6. look back, 7. repair
-  const uint32_t ep = kp.epoch;
-  TileSlot *slot = kp.slots + t;
-  uint64_t pexit = 0, pcnt = 0, pok = 0;
-  if (t == 0) {
-    if (tid == 0) {
-      st_agent(&slot->p[0], gran(ep, s_exit));
-      st_agent(&slot->p[1], gran(ep, s_n));
-      st_agent(&slot->p[2], gran(ep, okc));
-    }
-  } else {
-    if (tid == 0) {
-      st_agent(&slot->a[0], gran(ep, s_exit));
-      st_agent(&slot->a[1], gran(ep, s_entry == kNone ? 0ull : s_entry + 1));
-      st_agent(&slot->a[2], gran(ep, (uint64_t)s_n | ((uint64_t)okc << 24)));
-    }
-    if (wave == 0) {
-      Prefix pre{0, 0, 0};
-      bool ok = true;
-      if (t % kGroup == kGroup - 1) ok = publish_group(kp, t / kGroup);
-      Diag dg;
-      if (ok) ok = lookback(kp, t, pre, dg);
-      if (kp.stamps && lane == 0)
-        kp.stamps[(uint64_t)t * 8 + 7] = (uint64_t)dg.spins | ((uint64_t)dg.slides << 20) | ((uint64_t)dg.mism << 40);
-      if (lane == 0) {
-        s_abort = ok ? 0u : 1u;
-        s_pexit = pre.exit;
-        s_pcnt = pre.cnt;
-        s_pok = pre.ok;
-      }
-    }
-    __syncthreads();
-    if (s_abort) return;
-    pexit = s_pexit;
-    pcnt = s_pcnt;
-    pok = s_pok;
-    if (pexit != s_entry) {
-      // the speculation was wrong (or there is no record start here): redo from the truth
-      if (kp.stats && tid == 0) atomicAdd(&kp.stats[kStatRewalk], 1u);
-      if (wave == 0) {
-        uint32_t n = 0;
-        uint64_t ex = pexit;
-        if (pexit >= tile_lo && pexit < tile_hi) ex = walk_tile(kp, sw, srec, tile_lo, tile_hi, pexit, n);
-        if (lane == 0) {
-          s_n = n;
-          s_exit = ex;
-        }
-      }
-      __syncthreads();
-      okc = count_pass(kp, sw, srec, s_n, tile_lo, scnt);
-    }
-    if (tid == 0) {
-      st_agent(&slot->p[0], gran(ep, s_exit));
-      st_agent(&slot->p[1], gran(ep, pcnt + s_n));
-      st_agent(&slot->p[2], gran(ep, pok + okc));
-    }
-  }
-  const uint32_t n = s_n;
-  stamp(kp, t, 4);
-
-  // 8. totals (last tile)
-  if (t == kp.ntiles - 1 && tid == 0) {
-    const uint64_t tot_rec = pcnt + n, tot_ok = pok + okc;
-    uint32_t fl = 0;
-    if ((kp.rec_off || kp.recs || kp.rec_status) && tot_rec > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
-    if (kp.flows && tot_ok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
-    kp.summary->n_records = tot_rec;
-    kp.summary->n_flows = tot_ok;
-    kp.summary->consumed = s_exit;
-    kp.summary->flags = fl;
-    kp.summary->epoch = ep;
-  }
-
-  // 9. outputs at their global positions
-  const uint8_t *sb = (const uint8_t *)sw;
-  uint32_t slot_base = 0;
-#pragma unroll
-  for (int s = 0; s < kSlots; ++s) {
-    const uint32_t i = tid + (uint32_t)s * kBlock;
-    bool ok = false;
-    FlowWords f;
-    uint64_t p = 0;
-    if (i < n) {
-      const uint32_t rel = srec[i];
-      p = tile_lo + rel;
-      const uint32_t incl = hdr(sw, rel, 2, big);
-      TileReader r{sw, sb, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
-      const uint32_t st = decode<true>(r, incl, f);
-      ok = st == NPR_FLOW_OK;
-      const uint64_t idx = pcnt + i;
-      if (idx < kp.rec_cap) {
-        if (kp.rec_off) kp.rec_off[idx] = p;
-        if (kp.recs) {
-          uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
-          row[0] = p;
-          row[1] = (uint64_t)hdr(sw, rel, 0, big) | ((uint64_t)hdr(sw, rel, 1, big) << 32);
-          row[2] = (uint64_t)incl | ((uint64_t)hdr(sw, rel, 3, big) << 32);
-        }
-        if (kp.rec_status) kp.rec_status[idx] = (uint8_t)st;
-      }
-    }
-    const uint64_t bal = __ballot(ok);
-    if (ok && kp.flows) {
-      uint32_t rank = slot_base + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-      for (uint32_t v = 0; v < wave; ++v) rank += scnt[s][v];
-      const uint64_t fi = pok + rank;
-      if (fi < kp.flow_cap) {
-        const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
-        uint4 *dst = reinterpret_cast<uint4 *>(kp.flows + o * 8);
-        dst[0] = make_uint4(f.d[0], f.d[1], f.d[2], f.d[3]);
-        dst[1] = make_uint4(f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8));
-        if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) {
-          uint4 *d6 = reinterpret_cast<uint4 *>(kp.flows_v6 + o * 8);
-          d6[0] = make_uint4(f.v6[0], f.v6[1], f.v6[2], f.v6[3]);
-          d6[1] = make_uint4(f.v6[4], f.v6[5], f.v6[6], f.v6[7]);
-        }
-      }
-    }
-    slot_base += scnt[s][0] + scnt[s][1] + scnt[s][2] + scnt[s][3];
-  }
-  stamp(kp, t, 5);
-  if (kp.stamps && tid == 0) kp.stamps[(uint64_t)t * 8 + 6] = ((uint64_t)s_n << 32) | (pexit != s_entry ? 1u : 0u);
-}
-
-hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse_extract, dim3(p.ntiles), dim3(kBlock), 0, s, p);
-  return hipGetLastError();
-}
-
-// =============================================================================================
-// Persistent, software-pipelined kernel.  gridDim.x = G resident workgroups;
-// workgroup b owns tiles b, b+G, b+2G, ...  Iteration k overlaps three tiles:
-//   - registers receive tile k+1 from HBM (prefetch issued first, committed to LDS last);
-//   - phase A, wave 0: speculate + walk tile k;  wave 1: resolve tile k-1 (its aggregate was
-//     published one iteration ago; the look-back words were loaded at the top of the iteration)
-//     and write its records/flows;  wave 2: fold the group-level look-back window for wave 1;
-//   - phase B, all waves: decode tile k once (Ok flows parked in LDS in rank order), publish.
-// HBM latency and hand-off latency hide behind a whole tile of LDS work; no wave waits for a
-// store.  Inter-workgroup hand-offs use self-validating {tag, value} granules (agent scope).
-// =============================================================================================
-typedef unsigned int u32x4 __attribute__((__vector_size__(16)));  // the b128 buffer-load type
-
-constexpr int kParkFlows = 288;  // >= max Ok flows per tile: an Ok record spans >= 16 + 42 bytes
-constexpr int kPrefetch = (kStage / 16 + kBlock - 1) / kBlock;  // 16-B chunks per thread
-constexpr uint32_t kOrigMax = 1u << 18;   // speculation: plausible orig_len bound
-constexpr uint32_t kTsRefWindow = 1u << 26;  // speculation: |ts_sec - first record's ts_sec|
-
-struct PipeShared {
-  uint32_t data[kStage / 4 + 4];
-  uint16_t srec[2][kMaxRec];
-  uint32_t park[kParkFlows * 8];
-  uint8_t pstat[kMaxRec];
-  uint32_t scnt[kSlots][4];
-  uint64_t entry[2], exit[2];
-  uint32_t n[2], okc[2];
-  uint64_t pexit, pcnt, pok;
-  Seg l2;
-  uint32_t l2_state, l2_tag, slow, abort;
-};
-
-__device__ __forceinline__ void prefetch_tile(const ParseParams &kp, uint32_t t, u32x4 (&q)[kPrefetch],
-                                              bool valid = true) {
-  const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-  const uint64_t avail = valid && kp.len > tile_lo ? kp.len - tile_lo : 0;
-  uint32_t nbytes = avail < (uint64_t)kStage ? (uint32_t)avail : (uint32_t)kStage;
-  nbytes = (nbytes + 15u) & ~15u;  // 0 when !valid: every load is out of range, nothing is fetched
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + tile_lo), 0, (int)nbytes, 0x00020000);
-  // unconditional loads (chunks past the staged range are out of the descriptor's range -> 0):
-  // one load sequence with one consumer keeps hipcc's waitcnt tracking exact
-#pragma unroll
-  for (int i = 0; i < kPrefetch; ++i) {
-    const uint32_t c = threadIdx.x + (uint32_t)i * kBlock;
-    q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(c * 16u), 0, 0);
-  }
-}
-
-__device__ __forceinline__ void commit_tile(uint32_t *data, const u32x4 (&q)[kPrefetch]) {
-#pragma unroll
-  for (int i = 0; i < kPrefetch; ++i) {
-    const uint32_t c = threadIdx.x + (uint32_t)i * kBlock;
-    if (c < kStage / 16) *reinterpret_cast<u32x4 *>(&data[c * 4]) = q[i];
-  }
-  if (threadIdx.x < 4) data[kStage / 4 + threadIdx.x] = 0;
-}
-
-// ---- speculation in tile-relative 32-bit arithmetic (wave 0, 64 candidates per round) --------
-struct SpecCtx {
-  uint32_t avail;    // bytes of the input from tile_lo, saturated to 32 bits
-  bool exact_end;    // avail is exact (not saturated): q == avail means "chain ends at EOF"
-  uint32_t frac_max, ts_ref;
-  bool has_ref;
-  bool big;
-};
-
-__device__ __forceinline__ bool plaus2(const SpecCtx &c, uint32_t ts, uint32_t frac, uint32_t incl, uint32_t orig) {
-  return incl >= 1u && incl <= kInclMax && orig >= incl && orig <= kOrigMax && frac < c.frac_max &&
-         (!c.has_ref || ts - c.ts_ref + kTsRefWindow <= 2u * kTsRefWindow);
-}
-
-// 0 = implausible, 1 = weak (fewer than two further headers checkable), 2 = strong
-__device__ __forceinline__ int grade32(const SpecCtx &c, const uint32_t *w, uint32_t r) {
-  if (c.avail - r < 16) return 0;
-  uint32_t ts = hdr(w, r, 0, c.big);
-  const uint32_t incl = hdr(w, r, 2, c.big);
-  if (!plaus2(c, ts, hdr(w, r, 1, c.big), incl, hdr(w, r, 3, c.big))) return 0;
-  if (c.avail - r - 16 < incl) return 0;
-  uint32_t q = r + 16 + incl;
-  int ver = 0;
-  for (int hop = 0; hop < 3; ++hop) {
-    if (q == c.avail && c.exact_end) return 2;
-    if (q + 16 > (uint32_t)kStage) return ver >= 2 ? 2 : 1;
-    if (c.avail - q < 16) return ver >= 1 ? 2 : 1;
-    const uint32_t ts2 = hdr(w, q, 0, c.big), incl2 = hdr(w, q, 2, c.big);
-    if (!plaus2(c, ts2, hdr(w, q, 1, c.big), incl2, hdr(w, q, 3, c.big))) return 0;
-    if (ts2 - ts + kTsWindow > 2u * kTsWindow) return 0;
-    ++ver;
-    if (c.avail - q - 16 < incl2) return ver >= 2 ? 2 : 1;
-    ts = ts2;
-    q += 16 + incl2;
-  }
-  return 2;
-}
-
-// first strong candidate in [lo_rel, span), else the first weak one; kNone if neither (wave-uniform)
-__device__ uint64_t speculate_wave(const SpecCtx &c, const uint32_t *w, uint64_t tile_lo, uint32_t lo_rel,
-                                   uint32_t span) {
-  const uint32_t lane = threadIdx.x & 63u;
-  uint32_t weak = 0xffffffffu;
-  for (uint32_t base = lo_rel; base < span; base += 64) {
-    const uint32_t r = base + lane;
-    const int g = r < span ? grade32(c, w, r) : 0;
-    const uint64_t b2 = __ballot(g == 2);
-    if (b2) return tile_lo + base + (uint32_t)__builtin_ctzll(b2);
-    const uint64_t b1 = __ballot(g == 1);
-    if (weak == 0xffffffffu && b1) weak = base + (uint32_t)__builtin_ctzll(b1);
-  }
-  return weak == 0xffffffffu ? kNone : tile_lo + weak;
-}
-
-// ---- fast decode: Ethernet (no tag) / IPv4 (IHL 5) or IPv6 (no extension) / TCP or UDP -------
-// Branch-light: 17 aligned LDS words + v_alignbyte, static field offsets, status by selects.
-// Returns 0xff when the frame is not of that shape (the caller then runs the general decode).
 template <bool FIELDS>
 __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel, uint32_t n, FlowWords &f) {
   const uint32_t sh = rel & 3u;
@@ -1021,6 +280,7 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
   const bool v6 = etype == 0x86ddu && (b0 >> 4) == 6u && n >= 54u && (nh == 6u || nh == 17u);
   if (!(v4 || v6)) return 0xffu;
   const uint32_t n3 = n - 14u;
+  // IPv4 (IHL 5): wrapping u16 payload length; options/padding absent -> never a remainder
   const uint32_t length = v4 ? ((be16(16) - 20u) & 0xffffu) : be16(18);
   const uint32_t hl3 = v4 ? 20u : 40u;
   const uint32_t st3 = (n3 - hl3 < length) ? (v4 ? NPR_FLOW_L2_IPV4_INCOMPLETE : NPR_FLOW_L2_IPV6_INCOMPLETE)
@@ -1030,7 +290,7 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
   const uint32_t hv = v4 ? be16(46) : be16(66);
   const uint32_t ulen = v4 ? be16(38) : be16(58);
   const uint32_t thl = (hv >> 12) * 4u;
-  const uint32_t off = v4 ? 0u : 3u;  // IPv6 leaves are 3 codes after the IPv4 ones
+  const uint32_t off = v4 ? 0u : 3u;  // the IPv6 TCP/UDP leaves are 3 codes after the IPv4 ones
   uint32_t st4;
   if (proto == 6u)
     st4 = n4 < 14u ? NPR_FLOW_L3_IPV4_TCP_INCOMPLETE + off
@@ -1041,453 +301,795 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
           : (ulen < 8u || n4 - 8u < ulen - 8u) ? NPR_FLOW_L3_IPV4_UDP_INCOMPLETE + off
           : n4 != ulen ? (v4 ? (uint32_t)NPR_FLOW_L3_IPV4_UDP_REMAINDER : (uint32_t)NPR_FLOW_L3_IPV6_UDP_REMAINDER)
                        : 0u;
-  const uint32_t st = st3 ? st3 : st4;
   if (FIELDS) {
     const uint32_t sp = v4 ? be16(34) : be16(54), dp = v4 ? be16(36) : be16(56);
-    f.d[0] = v4 ? __builtin_amdgcn_alignbyte(a[7], a[6], 2) : 0u;  // src ip bytes 26..29
-    f.d[1] = v4 ? __builtin_amdgcn_alignbyte(a[8], a[7], 2) : 0u;  // dst ip bytes 30..33
+    f.d[0] = v4 ? __builtin_amdgcn_alignbyte(a[7], a[6], 2) : 0u;  // IPv4 src, bytes 26..29
+    f.d[1] = v4 ? __builtin_amdgcn_alignbyte(a[8], a[7], 2) : 0u;  // IPv4 dst, bytes 30..33
     f.d[2] = sp | (dp << 16);
     f.d[3] = a[1] & 0xffff0000u;  // vlan 0 | src mac 0..1
     f.d[4] = a[2];
     f.d[5] = a[0];
     f.d[6] = (a[1] & 0xffffu) | (((v6 ? NPR_FLOW_KIND_IPV6 : 0u) | (proto == 17u ? NPR_FLOW_KIND_UDP : 0u)) << 16);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) f.v6[k] = __builtin_amdgcn_alignbyte(a[6 + k], a[5 + k], 2);  // bytes 22..53
   }
-  return st;
+  return st3 ? st3 : st4;
 }
 
-// ---- raw look-back words, issued early and decoded late ------------------------------------
-struct RawWin {
-  uint64_t w[7];
-};
-
-// wave 1: the previous tile's group mates; wave 2: the groups before; others: a dummy word.
-// Every wave issues the same 7 loads so none of them is conditional.
-__device__ __forceinline__ void issue_window(const ParseParams &kp, uint32_t tp, bool has_prev, RawWin &r) {
-  const int lane = (int)(threadIdx.x & 63u), wave = (int)(threadIdx.x >> 6);
-  const uint32_t pg = tp / kGroup, pi = tp % kGroup;
-  const int64_t k = (int64_t)tp - 1 - lane;
-  const int64_t gg = (int64_t)pg - 1 - lane;
-  const bool tile_lane = has_prev && wave == 1 && lane < (int)pi;
-  const bool group_lane = has_prev && wave == 2 && gg >= 0;
-  const TileSlot *ts = kp.slots + (group_lane ? gg * kGroup + kGroup - 1 : (tile_lane ? k : 0));
-  const uint64_t *ext = group_lane ? kp.groups[gg].g : ts->a;
-  r.w[0] = ld_agent(&ts->p[0]);
-  r.w[1] = ld_agent(&ts->p[1]);
-  r.w[2] = ld_agent(&ts->p[2]);
-  r.w[3] = ld_agent(ext + 0);
-  r.w[4] = ld_agent(ext + 1);
-  r.w[5] = ld_agent(ext + 2);
-  r.w[6] = ld_agent(group_lane ? ext + 3 : &ts->p[0]);
-}
-__device__ __forceinline__ LaneSeg decode_tile_lanes(const ParseParams &kp, int64_t k, bool inr, const RawWin &r) {
-  LaneSeg L{};
-  L.first = L.last = k;
-  L.mism = -1;
-  L.valid = true;
-  if (!inr) return L;
-  const uint32_t ep = kp.epoch;
-  if (tagged(r.w[0], ep) && tagged(r.w[1], ep) && tagged(r.w[2], ep)) {
-    L.present = L.anchor = true;
-    L.exit = r.w[0] & kMask48; L.cnt = r.w[1] & kMask48; L.ok = r.w[2] & kMask48;
-  } else if (tagged(r.w[3], ep) && tagged(r.w[4], ep) && tagged(r.w[5], ep)) {
-    L.present = true;
-    const uint64_t e1 = r.w[4] & kMask48, c = r.w[5] & kMask48;
-    L.entry = e1 ? e1 - 1 : kNone;
-    L.exit = r.w[3] & kMask48;
-    L.cnt = c & 0xffffffull;
-    L.ok = (c >> 24) & 0xffffffull;
-  }
-  return L;
-}
-__device__ __forceinline__ LaneSeg decode_group_lanes(const ParseParams &kp, int64_t gg, bool inr, const RawWin &r) {
-  LaneSeg L{};
-  L.first = gg * kGroup;
-  L.last = gg * kGroup + kGroup - 1;
-  L.mism = -1;
-  L.valid = true;
-  if (!inr) return L;
-  const uint32_t ep = kp.epoch;
-  if (tagged(r.w[0], ep) && tagged(r.w[1], ep) && tagged(r.w[2], ep)) {
-    L.present = L.anchor = true;
-    L.exit = r.w[0] & kMask48; L.cnt = r.w[1] & kMask48; L.ok = r.w[2] & kMask48;
-  } else if (tagged(r.w[3], ep) && tagged(r.w[4], ep) && tagged(r.w[5], ep) && tagged(r.w[6], ep)) {
-    L.present = true;
-    const uint64_t e1 = r.w[4] & kMask48, w3 = r.w[6] & kMask48;
-    L.entry = e1 ? e1 - 1 : kNone;
-    L.exit = r.w[3] & kMask48;
-    L.cnt = r.w[5] & kMask48;
-    L.ok = w3 & ((1ull << 40) - 1);
-    L.valid = (w3 >> 40) & 1ull;
-    L.anchor = (w3 >> 41) & 1ull;
-    L.mism = L.valid ? -1 : L.first + (int64_t)((w3 >> 42) & 63ull);
-  }
-  return L;
-}
-
-enum : uint32_t { kWinFail = 0, kWinResolved = 1, kWinAgg = 2, kWinEmpty = 3, kWinAnchored = 4 };
-
-// one record of the tile -> status (+ flow words); fast shape first, general decoder otherwise
-__device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *data, uint64_t tile_lo,
+// one record (header at LDS offset rel) -> status (+ flow words); fast shape first
+template <bool FIELDS>
+__device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo,
                                                uint32_t rel, FlowWords &f) {
-  const uint32_t incl = hdr(data, rel, 2, kp.big);
-  uint32_t st = decode_fast<true>(data, rel + 16u, incl, f);
+  const uint32_t incl = hdr(w, rel, 2, kp.big);
+  uint32_t st = decode_fast<FIELDS>(w, rel + 16u, incl, f);
   if (st == 0xffu) {
     const uint64_t p = tile_lo + rel;
-    TileReader r{data, (const uint8_t *)data, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
-    st = decode<true>(r, incl, f);
+    TileReader r{w, (const uint8_t *)w, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
+    st = decode<FIELDS>(r, incl, f);
   }
   return st;
 }
 
-// Phase B: decode every record of the tile once: status -> pstat, Ok flows -> park (rank order).
-// `direct` (slow path) writes the flows straight to their global positions instead.
-__device__ uint32_t decode_tile(const ParseParams &kp, PipeShared &sh, uint64_t tile_lo, int slot, bool direct,
-                                uint64_t pok) {
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t n = sh.n[slot];
-  uint32_t base = 0;
-  for (int s = 0; s < kSlots; ++s) {
-    if ((uint32_t)s * kBlock >= n) break;  // uniform
-    const uint32_t i = tid + (uint32_t)s * kBlock;
-    FlowWords f;
-    bool ok = false;
-    uint64_t p = 0;
-    if (i < n) {
-      const uint32_t rel = sh.srec[slot][i];
-      p = tile_lo + rel;
-      const uint32_t st = decode_rec(kp, sh.data, tile_lo, rel, f);
-      if (!direct) sh.pstat[i] = (uint8_t)st;
-      else if (kp.rec_status && kp.pcnt_slow + i < kp.rec_cap) kp.rec_status[kp.pcnt_slow + i] = (uint8_t)st;
-      ok = st == NPR_FLOW_OK;
-    }
-    const uint64_t bal = __ballot(ok);
-    if (lane == 0) sh.scnt[s][wave] = (uint32_t)__builtin_popcountll(bal);
-    __syncthreads();
-    if (ok) {
-      uint32_t rank = base + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-      for (uint32_t v = 0; v < wave; ++v) rank += sh.scnt[s][v];
-      const u32x4 lo4 = u32x4{f.d[0], f.d[1], f.d[2], f.d[3]};
-      const u32x4 hi4 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
-      if (!direct) {
-        u32x4 *dst = reinterpret_cast<u32x4 *>(&sh.park[rank * 8]);
-        dst[0] = lo4;
-        dst[1] = hi4;
-      } else if (kp.flows && pok + rank < kp.flow_cap) {
-        const uint64_t o = kp.flow_cap - 1 - (pok + rank);
-        u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-        dst[0] = lo4;
-        dst[1] = hi4;
-        if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) {
-          GlobalReader gr{kp.buf + p + 16, kp.len - p - 16};
-          FlowWords g;
-          decode<true>(gr, hdr(sh.data, (uint32_t)(p - tile_lo), 2, kp.big), g);
-          u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
-          d6[0] = u32x4{g.v6[0], g.v6[1], g.v6[2], g.v6[3]};
-          d6[1] = u32x4{g.v6[4], g.v6[5], g.v6[6], g.v6[7]};
-        }
-      }
-    }
-    base += sh.scnt[s][0] + sh.scnt[s][1] + sh.scnt[s][2] + sh.scnt[s][3];
-    __syncthreads();  // scnt is reused by the next slot
+// ---------------------------------------------------------------------------------------------
+// hand-off granules (MI355X_MICROARCH.md "R2": the data IS the flag, {tag, value} 8-B)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t gran(uint32_t tag, uint64_t v) { return ((uint64_t)tag << 48) | (v & kMask48); }
+__device__ __forceinline__ void st_agent(uint64_t *p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool tagged(uint64_t w, uint32_t ep) { return (w >> 48) == ep; }
+__device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// A segment of consecutive tiles [first, last] under speculation.
+struct Seg {
+  uint64_t entry, exit, cnt, ok;
+  int64_t first, last, mism;  // mism: lowest tile whose speculated entry is contradicted
+  bool valid;
+};
+
+__device__ __forceinline__ uint64_t tile_end(const ParseParams &kp, int64_t k) {
+  const uint64_t e = kp.org + (uint64_t)(k + 1) * kTile;
+  return e < kp.len ? e : kp.len;
+}
+
+// Chain-consistency monoid: X then Y (Y's tiles follow X's).  Y's counts are trusted only when
+// Y's speculated entry is exactly where X's chain continues.
+__device__ __forceinline__ Seg combine(const ParseParams &kp, const Seg &X, const Seg &Y) {
+  Seg r = X;
+  r.last = Y.last;
+  if (!X.valid) return r;                       // keep the lowest mismatch
+  if (X.exit < tile_end(kp, X.last)) return r;  // chain ended inside X (Q3): Y is moot
+  if (X.exit >= tile_end(kp, Y.last)) return r; // one record spans all of Y: no record starts there
+  if (X.exit != Y.entry) {                      // Y's speculated start is wrong
+    r.valid = false;
+    r.mism = Y.first;
+    return r;
   }
-  return base;
+  r.exit = Y.exit;
+  r.cnt = X.cnt + Y.cnt;
+  r.ok = X.ok + Y.ok;
+  r.valid = Y.valid;
+  r.mism = Y.mism;
+  return r;
 }
 
-__device__ __forceinline__ void write_summary(const ParseParams &kp, uint64_t tot_rec, uint64_t tot_ok, uint64_t consumed) {
-  uint32_t fl = 0;
-  if ((kp.rec_off || kp.recs || kp.rec_status) && tot_rec > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
-  if (kp.flows && tot_ok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
-  kp.summary->n_records = tot_rec;
-  kp.summary->n_flows = tot_ok;
-  kp.summary->consumed = consumed;
-  kp.summary->flags = fl;
-  kp.summary->epoch = kp.epoch;
-}
-
-// dense record rows [i0, n) of a tile (record offsets from srec)
-__device__ __forceinline__ void write_records(const ParseParams &kp, const uint16_t *srec, uint32_t n,
-                                              uint64_t tile_lo, uint64_t pcnt, const uint8_t *pstat,
-                                              uint32_t i0, uint32_t step) {
-  for (uint32_t i = i0; i < n; i += step) {
-    const uint64_t idx = pcnt + i;
-    if (idx >= kp.rec_cap) break;
-    const uint64_t p = tile_lo + srec[i];
-    if (kp.rec_off) kp.rec_off[idx] = p;
-    if (kp.rec_status && pstat) kp.rec_status[idx] = pstat[i];
-    if (kp.recs) {
-      GlobalReader gr{kp.buf + p, kp.len - p};
-      const uint32_t h0 = gr.le32(0), h1 = gr.le32(4), h2 = gr.le32(8), h3 = gr.le32(12);
-      const bool big = kp.big;
-      uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
-      row[0] = p;
-      row[1] = (uint64_t)(big ? __builtin_bswap32(h0) : h0) | ((uint64_t)(big ? __builtin_bswap32(h1) : h1) << 32);
-      row[2] = (uint64_t)(big ? __builtin_bswap32(h2) : h2) | ((uint64_t)(big ? __builtin_bswap32(h3) : h3) << 32);
-    }
+// Bounded wait: false once the grid aborted or this wait exceeded the time budget.
+__device__ __forceinline__ bool spin_ok(const ParseParams &kp, uint64_t t0) {
+  __builtin_amdgcn_s_sleep(2);
+  if (__hip_atomic_load(kp.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kp.epoch) return false;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
+    __hip_atomic_store(kp.abort_word, kp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
   }
+  return true;
 }
 
-__global__ __launch_bounds__(kBlock) void k_parse_pipe(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) PipeShared sh;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  if (b >= kp.ntiles) return;
-  const uint32_t nmine = (kp.ntiles - 1 - b) / G + 1;
+// One lane's element of a 64-wide fold: a tile aggregate (level 0), a 64-tile group aggregate
+// (level 1) or a 4096-tile block aggregate (level 2).
+struct LaneSeg {
+  uint64_t entry, exit, cnt, ok;
+  int64_t first, last, mism;
+  bool valid, present;
+};
+
+// level 0: A = {exit, entry + 1, n | okc << 24};  levels 1/2: {exit, entry + 1, cnt, ok | valid << 32 | mism_rel << 33}
+__device__ __forceinline__ LaneSeg load_agg(const ParseParams &kp, int lvl, int64_t idx, bool inr) {
+  LaneSeg L{};
+  L.mism = -1;
+  L.valid = true;
+  const int sh = 6 * lvl;
+  L.first = idx << sh;
+  const int64_t last = ((idx + 1) << sh) - 1;
+  L.last = last < (int64_t)kp.ntiles - 1 ? last : (int64_t)kp.ntiles - 1;
+  if (!inr) return L;
   const uint32_t ep = kp.epoch;
+  const uint64_t *w = lvl == 0 ? kp.slots[idx].a : (lvl == 1 ? kp.groups1[idx].g : kp.groups2[idx].g);
+  const uint64_t w0 = ld_agent(w + 0), w1 = ld_agent(w + 1), w2 = ld_agent(w + 2);
+  const uint64_t w3 = lvl == 0 ? w0 : ld_agent(w + 3);
+  L.present = tagged(w0, ep) && tagged(w1, ep) && tagged(w2, ep) && tagged(w3, ep);
+  const uint64_t e1 = w1 & kMask48;
+  L.entry = e1 ? e1 - 1 : kNone;
+  L.exit = w0 & kMask48;
+  if (lvl == 0) {
+    L.cnt = w2 & 0xffffffull;
+    L.ok = (w2 >> 24) & 0xffffffull;
+  } else {
+    const uint64_t v3 = w3 & kMask48;
+    L.cnt = w2 & kMask48;
+    L.ok = v3 & 0xffffffffull;
+    L.valid = (v3 >> 32) & 1ull;
+    L.mism = L.valid ? -1 : L.first + (int64_t)((v3 >> 33) & 0x7fffull);
+  }
+  return L;
+}
 
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1);
+  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
+    v += ((uint64_t)hi << 32) | lo;
+  }
+  return v;
+}
+
+// Fold lanes [lo .. 0] (ascending tile order = descending lane) into one segment.  Fast path:
+// every link consistent, no END, no pass-through, all valid -> two wave sums; otherwise the
+// serial monoid (wave-uniform, readlane).
+__device__ Seg fold_window(const ParseParams &kp, const LaneSeg &L, int lo) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const uint64_t prev_exit = shfl_down64(L.exit);  // exit of the preceding segment (lane + 1)
+  const bool inr = lane <= lo;
+  const bool bad = lane < lo && (!L.valid || L.entry != prev_exit);
+  const bool endc = inr && L.exit < tile_end(kp, L.last);
+  const bool lo_bad = lane == lo && !L.valid;
+  Seg r;
+  if (__ballot(bad || endc || lo_bad) == 0ull) {
+    r.cnt = wave_sum64(inr ? L.cnt : 0ull);
+    r.ok = wave_sum64(inr ? L.ok : 0ull);
+    r.entry = rl64(L.entry, lo);
+    r.exit = rl64(L.exit, 0);
+    r.first = (int64_t)rl64((uint64_t)L.first, lo);
+    r.last = (int64_t)rl64((uint64_t)L.last, 0);
+    r.mism = -1;
+    r.valid = true;
+    return r;
+  }
+  const uint64_t bval = __ballot(L.valid);
+  auto lane_seg = [&](int j) {
+    Seg y;
+    y.entry = rl64(L.entry, j);
+    y.exit = rl64(L.exit, j);
+    y.cnt = rl64(L.cnt, j);
+    y.ok = rl64(L.ok, j);
+    y.first = (int64_t)rl64((uint64_t)L.first, j);
+    y.last = (int64_t)rl64((uint64_t)L.last, j);
+    y.mism = (int64_t)rl64((uint64_t)L.mism, j);
+    y.valid = (bval >> j) & 1ull;
+    return y;
+  };
+  r = lane_seg(lo);
+  for (int j = lo - 1; j >= 0; --j) r = combine(kp, r, lane_seg(j));
+  return r;
+}
+
+// Load + fold `cnt` (1..64) consecutive level-`lvl` aggregates starting at element `base`
+// (wave-uniform).  Waits (bounded) until all are published.
+__device__ bool fold_range(const ParseParams &kp, int lvl, int64_t base, int cnt, Seg &out, uint64_t t0) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const bool inr = lane < cnt;
+  for (;;) {
+    const LaneSeg L = load_agg(kp, lvl, base + cnt - 1 - lane, inr);
+    if (__ballot(inr && !L.present) == 0ull) {
+      out = fold_window(kp, L, cnt - 1);
+      return true;
+    }
+    if (!spin_ok(kp, t0)) return false;
+  }
+}
+
+// Exact prefix through tile m: its P granules (published by k_emit_tiles), bounded wait.
+__device__ bool wait_exact(const ParseParams &kp, int64_t m, Seg &X, uint64_t t0) {
+  const TileSlot *s = kp.slots + m;
+  for (;;) {
+    const uint64_t p0 = ld_agent(&s->p[0]), p1 = ld_agent(&s->p[1]), p2 = ld_agent(&s->p[2]);
+    if (tagged(p0, kp.epoch) && tagged(p1, kp.epoch) && tagged(p2, kp.epoch)) {
+      X.exit = p0 & kMask48;
+      X.cnt = p1 & kMask48;
+      X.ok = p2 & kMask48;
+      X.first = 0;
+      X.last = m;
+      X.mism = -1;
+      X.valid = true;
+      return true;
+    }
+    if (!spin_ok(kp, t0)) return false;
+  }
+}
+
+__device__ __forceinline__ Seg start_seg(const ParseParams &kp) {
+  Seg X;
+  X.entry = X.exit = kp.start;
+  X.cnt = X.ok = 0;
+  X.first = X.last = -1;
+  X.mism = -1;
+  X.valid = true;
+  return X;
+}
+
+// Generic exact prefix of tiles [a, t) continuing X (wave 0): ascending, largest aligned
+// aggregates first; every contradiction is settled by the exact prefix of the offending tile.
+__device__ bool prefix_generic(const ParseParams &kp, Seg X, int64_t a, int64_t t, Seg &out, uint64_t t0) {
+  for (;;) {
+    if (!X.valid) {
+      const int64_t m = X.mism;
+      if (!wait_exact(kp, m, X, t0)) return false;
+      if (kp.stats && (threadIdx.x & 63u) == 0) atomicAdd(kp.stats + kStatMismWait, 1u);
+      a = m + 1;
+    }
+    if (a >= t) break;
+    int lvl;
+    int64_t cnt;
+    if ((a & 4095) == 0 && t - a >= 4096) {
+      lvl = 2;
+      cnt = (t - a) >> 12;
+    } else if ((a & 63) == 0 && t - a >= 64) {
+      lvl = 1;
+      cnt = (t - a) >> 6;
+      const int64_t to_blk = (4096 - (a & 4095)) >> 6;
+      cnt = cnt < to_blk ? cnt : to_blk;
+    } else {
+      lvl = 0;
+      cnt = t - a;
+      const int64_t to_grp = 64 - (a & 63);
+      cnt = cnt < to_grp ? cnt : to_grp;
+    }
+    cnt = cnt < 64 ? cnt : 64;
+    Seg Y;
+    if (!fold_range(kp, lvl, a >> (6 * lvl), (int)cnt, Y, t0)) return false;
+    X = combine(kp, X, Y);
+    a += cnt << (6 * lvl);
+  }
+  out = X;
+  return true;
+}
+
+// ---------------------------------------------------------------------------------------------
+// speculation (tile-relative 32-bit arithmetic) + chain walk
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kOrigMax = 1u << 18;       // plausible orig_len bound
+constexpr uint32_t kTsRefWindow = 1u << 26;   // |ts_sec - the first record's ts_sec| (~2 years)
+
+struct SpecCtx {
+  uint32_t avail;    // bytes of the input from tile_lo, saturated to 32 bits
+  bool exact_end;    // avail is exact: q == avail means "the chain ends exactly at EOF"
+  uint32_t frac_max, ts_ref;
+  bool has_ref, big;
+};
+
+__device__ __forceinline__ bool plaus(const SpecCtx &c, uint32_t ts, uint32_t frac, uint32_t incl, uint32_t orig) {
+  return incl >= 1u && incl <= kInclMax && orig >= incl && orig <= kOrigMax && frac < c.frac_max &&
+         (!c.has_ref || ts - c.ts_ref + kTsRefWindow <= 2u * kTsRefWindow);
+}
+
+// How plausible is LDS offset r as a record start?  0 = no; 1 = weak (its header passes but
+// fewer than two chained headers could be checked inside the staged window); 2 = strong.
+// A heuristic only: k_emit_tiles verifies every guess; a wrong one costs a wait, never a result.
+__device__ __forceinline__ int grade(const SpecCtx &c, const uint32_t *w, uint32_t r) {
+  if (c.avail - r < 16) return 0;
+  uint32_t ts = hdr(w, r, 0, c.big);
+  const uint32_t incl = hdr(w, r, 2, c.big);
+  if (!plaus(c, ts, hdr(w, r, 1, c.big), incl, hdr(w, r, 3, c.big))) return 0;
+  if (c.avail - r - 16 < incl) return 0;
+  uint32_t q = r + 16 + incl;
+  int ver = 0;
+  for (int hop = 0; hop < 3; ++hop) {
+    if (q == c.avail && c.exact_end) return 2;
+    if (q + 16 > (uint32_t)kStage) return ver >= 2 ? 2 : 1;
+    if (c.avail - q < 16) return ver >= 1 ? 2 : 1;
+    const uint32_t ts2 = hdr(w, q, 0, c.big), incl2 = hdr(w, q, 2, c.big);
+    if (!plaus(c, ts2, hdr(w, q, 1, c.big), incl2, hdr(w, q, 3, c.big))) return 0;
+    if (ts2 - ts + kTsWindow > 2u * kTsWindow) return 0;
+    ++ver;
+    if (c.avail - q - 16 < incl2) return ver >= 2 ? 2 : 1;
+    ts = ts2;
+    q += 16 + incl2;
+  }
+  return 2;
+}
+
+// PcapRecords::parse loop (src/record.rs:30-49) over one tile, from `entry`, by one wave.
+// Records whose header starts before tile_hi belong to this tile.  Returns the exit: the first
+// chain offset >= tile_hi, or (chain END, Q3) the offset of the first incomplete record.
+// Stride speculation: while the record length repeats, lane j confirms records j, j+64, j+128,
+// j+192 ahead in one LDS round trip (up to 256 records per step); one record per step otherwise.
+constexpr int kWalkUnroll = 4;
+__device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
+                              uint64_t tile_hi, uint64_t entry, uint32_t &n_out) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool big = kp.big;
+  const uint32_t span = (uint32_t)(tile_hi - tile_lo);
+  const uint64_t av = kp.len - tile_lo;
+  const uint32_t avail = av > 0xffffffffull ? 0xffffffffu : (uint32_t)av;  // bytes from tile_lo
+  uint64_t p = entry;
+  uint32_t n = 0;
+  while (p < tile_hi) {
+    const uint32_t r = (uint32_t)(p - tile_lo);
+    const uint32_t incl = hdr(w, r, 2, big);
+    if (kp.len - p < 16 || kp.len - p - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
+    if (incl > (uint32_t)kTile) {  // a record longer than a tile: no stride to speculate on
+      if (lane == 0) srec[n] = (uint16_t)r;
+      n += 1;
+      p += 16ull + incl;
+      continue;
+    }
+    const uint32_t stride = 16u + incl;
+    uint64_t b[kWalkUnroll];
+    uint32_t qr[kWalkUnroll];
+#pragma unroll
+    for (int u = 0; u < kWalkUnroll; ++u) {
+      const uint32_t k = lane + 64u * (uint32_t)u;
+      qr[u] = r + k * stride;  // < 2^24: k < 256, stride <= 16 + kTile
+      bool ok = k == 0;
+      if (k != 0 && qr[u] < span) ok = hdr(w, qr[u], 2, big) == incl && avail - qr[u] >= stride;
+      b[u] = __ballot(ok);
+    }
+    uint32_t m = 0;
+#pragma unroll
+    for (int u = 0; u < kWalkUnroll; ++u) {
+      if (m != 64u * (uint32_t)u) break;
+      m += (~b[u] == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~b[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < kWalkUnroll; ++u)
+      if (lane + 64u * (uint32_t)u < m) srec[n + lane + 64u * (uint32_t)u] = (uint16_t)qr[u];
+    n += m;
+    p += (uint64_t)m * stride;
+  }
+  n_out = n;
+  return p;
+}
+
+__device__ __forceinline__ void stamp(const ParseParams &kp, uint32_t t, int k) {
+  if (kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * 8 + k] = __builtin_amdgcn_s_memrealtime();
+}
+
+// LDS written by some lanes of this wave, then read by others: LDS executes one wave's requests
+// in order, so only the compiler must not move the accesses across this point.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
+constexpr int kChunks = (kStage / 16 + kWave - 1) / kWave;  // 16-B staging loads per lane
+
+// Stage tile t ([tile_lo, tile_lo + kStage) clipped to the input) into registers: one buffer
+// descriptor whose range ends at the input end (or the stage end), so chunks past it read 0.
+__device__ __forceinline__ void stage_issue(const ParseParams &kp, uint64_t tile_lo, u32x4 (&q)[kChunks]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t avail = kp.len > tile_lo ? kp.len - tile_lo : 0;
+  const uint32_t nbytes = avail < (uint64_t)kStage ? (uint32_t)avail : (uint32_t)kStage;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + tile_lo), 0, (int)((nbytes + 15u) & ~15u), 0x00020000);
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i)
+    q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((lane + 64u * (uint32_t)i) * 16u), 0, 0);
+}
+__device__ __forceinline__ void stage_commit(uint32_t *data, const u32x4 (&q)[kChunks]) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int i = 0; i < kChunks; ++i) {
+    const uint32_t c = lane + 64u * (uint32_t)i;
+    if (c < kStage / 16) *reinterpret_cast<u32x4 *>(&data[c * 4]) = q[i];
+  }
+  if (lane < 4) data[kStage / 4 + lane] = 0;
+}
+
+// speculation context of this launch: ts_usec bound from the file magic, the first record's
+// ts_sec as a reference (both read once per wave)
+__device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
   SpecCtx sc;
   sc.big = kp.big;
   sc.frac_max = kp.frac_max;
-  sc.has_ref = false;
-  sc.ts_ref = 0;
-  if (kp.flags & kFlagMagicAtZero) {  // pcap magic: microsecond captures bound ts_usec < 1e6
-    const uint32_t m = *reinterpret_cast<const uint32_t *>(kp.buf);
+  if (kp.flags & kFlagMagicAtZero) {  // microsecond pcap magic: ts_usec < 1e6
+    GlobalReader gm{kp.buf, 4};
+    const uint32_t m = gm.le32(0);
     if (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u) sc.frac_max = 1000000u;
   }
-  if (!(kp.flags & kFlagSpecFirst) && kp.len >= kp.start + 16) {  // the first record's ts_sec
-    GlobalReader gr{kp.buf + kp.start, 4};
-    const uint32_t v = gr.le32(0);
-    sc.ts_ref = kp.big ? __builtin_bswap32(v) : v;
-    sc.has_ref = true;
-  }
-  u32x4 q[kPrefetch];
-  prefetch_tile(kp, b, q);
-  commit_tile(sh.data, q);
-  if (tid == 0) {
-    sh.abort = 0;
-    sh.l2_tag = 0xffffffffu;
-  }
-  __syncthreads();
+  sc.has_ref = kp.len >= kp.start + 16;
+  GlobalReader gr{kp.buf + kp.start, sc.has_ref ? 4ull : 0ull};
+  const uint32_t v = gr.le32(0);
+  sc.ts_ref = kp.big ? __builtin_bswap32(v) : v;
+  sc.avail = 0;
+  sc.exact_end = true;
+  return sc;
+}
 
-  for (uint32_t k = 0; k <= nmine; ++k) {
-    const bool has_cur = k < nmine, has_prev = k >= 1, has_next = k + 1 < nmine;
-    const uint32_t t = b + k * G, tp = t - G;
-    const int cur = (int)(k & 1u), prv = cur ^ 1;
+// first strong (else first weak) record-start candidate in [0, span) of the staged tile, 64
+// candidates per round; kNone if neither (wave-uniform)
+__device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t span) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t avail = kp.len - tile_lo;
+  sc.avail = avail > 0xffffffffull ? 0xffffffffu : (uint32_t)avail;
+  sc.exact_end = avail <= 0xffffffffull;
+  uint32_t weak = 0xffffffffu;
+  for (uint32_t base = 0; base < span; base += 64) {
+    const uint32_t r = base + lane;
+    const int g = r < span ? grade(sc, w, r) : 0;
+    const uint64_t b2 = __ballot(g == 2);
+    if (b2) return tile_lo + base + (uint32_t)__builtin_ctzll(b2);
+    const uint64_t b1 = __ballot(g == 1);
+    if (weak == 0xffffffffu && b1) weak = base + (uint32_t)__builtin_ctzll(b1);
+  }
+  return weak == 0xffffffffu ? kNone : tile_lo + weak;
+}
+
+struct ParseShared {  // one wave's LDS
+  uint32_t data[kStage / 4 + 4];
+  uint16_t srec[kMaxRec];
+};
+
+__device__ __forceinline__ void publish_fold(const ParseParams &kp, GroupSlot *G, const Seg &c, int64_t first) {
+  const uint32_t ep = kp.epoch;
+  const uint64_t mrel = c.valid ? 0ull : (uint64_t)(c.mism - first) & 0x7fffull;
+  st_agent(&G->g[0], gran(ep, c.exit));
+  st_agent(&G->g[1], gran(ep, c.entry == kNone ? 0ull : c.entry + 1));
+  st_agent(&G->g[2], gran(ep, c.cnt));
+  st_agent(&G->g[3], gran(ep, (c.ok & 0xffffffffull) | ((uint64_t)c.valid << 32) | (mrel << 33)));
+}
+
+// contiguous tile range [c0, c1) of worker w out of W (balanced)
+__device__ __forceinline__ void chunk_of(uint32_t nt, uint32_t w, uint32_t W, uint32_t &c0, uint32_t &c1) {
+  c0 = (uint32_t)((uint64_t)w * nt / W);
+  c1 = (uint32_t)((uint64_t)(w + 1) * nt / W);
+}
+
+__device__ __forceinline__ uint32_t group_size(const ParseParams &kp, uint32_t g) {
+  return kp.ntiles - (g << 6) < 64u ? kp.ntiles - (g << 6) : 64u;
+}
+
+// group g's last arriver: G1(g), and when g is the last group of block h to finish, G2(h)
+__device__ __forceinline__ void fold_groups(const ParseParams &kp, uint32_t g) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  Seg c;
+  if (!fold_range(kp, 0, (int64_t)g << 6, (int)group_size(kp, g), c, t0)) return;
+  uint32_t last2 = 0;
+  const uint32_t h = g >> 6;
+  const uint32_t hsize = kp.ngroups1 - (h << 6) < 64u ? kp.ngroups1 - (h << 6) : 64u;
+  if (lane == 0) {
+    publish_fold(kp, kp.groups1 + g, c, (int64_t)g << 6);
+    __hip_atomic_store(kp.cnt1 + 2 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last2 = __hip_atomic_fetch_add(kp.cnt2 + 2 * h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hsize - 1u;
+  }
+  if (__builtin_amdgcn_readfirstlane(last2) && fold_range(kp, 1, (int64_t)h << 6, (int)hsize, c, t0) && lane == 0) {
+    publish_fold(kp, kp.groups2 + h, c, (int64_t)h << 12);
+    __hip_atomic_store(kp.cnt2 + 2 * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 1: scan_chunk — ONE WAVE owns the contiguous tiles [c0, c1) and never waits on another
+// wave (no workgroup barriers anywhere).  Per tile: (tile + 2 -> registers) | entry = the
+// previous tile's exit while the chain continues, else a speculated start | walk -> record
+// offsets, also kept in the offset scratch for pass 2 | status-only decode -> Ok count |
+// publish A = {entry, exit, n, Ok count} and arrive at the group counter.  The arrival's
+// returned value is consumed one tile later (its round trip overlaps the next tile): the last
+// arriver of a 64-tile group folds G1, the last group of a 4096-tile block folds G2.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  // two tiles in flight: register sets qa / qb alternate (the loop is unrolled by two so the
+  // compiler counts the loads it waits for)
+  u32x4 qa[kChunks], qb[kChunks];
+  stage_issue(kp, kp.org + (uint64_t)c0 * kTile, qa);
+  if (c0 + 1 < c1) stage_issue(kp, kp.org + (uint64_t)(c0 + 1) * kTile, qb);
+  const SpecCtx sc = spec_ctx(kp);
+  uint64_t carry = kNone;                          // exact continuation of the chain
+  uint32_t arrived = 0xffffffffu, arrived_g = 0;   // lane 0: pending group-counter arrival
+  auto step = [&](uint32_t t, u32x4 (&q)[kChunks]) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
-    const uint64_t ptile_lo = kp.org + (uint64_t)tp * kTile;
-    if (kp.stamps && has_cur && tid == 0) kp.stamps[(uint64_t)t * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    stamp(kp, t, 0);
+    stage_commit(sh.data, q);
+    wave_sync();
+    if (t + 2 < c1) stage_issue(kp, tile_lo + 2ull * kTile, q);
 
-    // (1) next tile -> registers;  (2) look-back words of the previous tile
-    prefetch_tile(kp, has_next ? t + G : b, q, has_next);
-    RawWin win;
-    issue_window(kp, has_prev ? tp : 0u, has_prev, win);
+    uint64_t entry = carry;
+    if (t == 0) {
+      entry = kp.start;
+    } else if (carry == kNone) {
+      entry = speculate(sc, kp, sh.data, tile_lo, (uint32_t)(tile_hi - tile_lo));
+      if (kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
+    }
+    stamp(kp, t, 1);
+    uint32_t n = 0;
+    uint64_t ex = entry == kNone ? 0ull : entry;
+    if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, entry, n);
+    wave_sync();
+    stamp(kp, t, 2);
 
-    // ---- phase A ----------------------------------------------------------------------------
-    if (wave == 0) {
-      if (has_cur) {  // speculate + walk tile t
-        const bool exact = t == 0 && !(kp.flags & kFlagSpecFirst);
-        uint64_t entry = kp.start;
-        if (!exact) {
-          const uint64_t avail = kp.len - tile_lo;
-          sc.avail = avail > 0xffffffffull ? 0xffffffffu : (uint32_t)avail;
-          sc.exact_end = avail <= 0xffffffffull;
-          const uint64_t lo = (t == 0) ? kp.start : tile_lo;
-          entry = speculate_wave(sc, sh.data, tile_lo, (uint32_t)(lo - tile_lo), (uint32_t)(tile_hi - tile_lo));
-        }
-        if (kp.stamps && lane == 0) kp.stamps[(uint64_t)t * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-        uint32_t n = 0;
-        uint64_t ex = entry;
-        if (entry != kNone && entry >= tile_lo && entry < tile_hi)
-          ex = walk_tile(kp, sh.data, sh.srec[cur], tile_lo, tile_hi, entry, n);
-        else if (entry == kNone)
-          ex = 0;
-        if (lane == 0) {
-          sh.n[cur] = n;
-          sh.entry[cur] = entry;
-          sh.exit[cur] = ex;
-        }
-        if (kp.stamps && lane == 0) kp.stamps[(uint64_t)t * 8 + 5] = __builtin_amdgcn_s_memrealtime();
+    // ---- offsets -> scratch (pairs of u16); Ok count (status-only decode)
+    if (kp.srec_g) {
+      uint32_t *dst = reinterpret_cast<uint32_t *>(kp.srec_g + (uint64_t)t * kMaxRec);
+      const uint32_t *src = reinterpret_cast<const uint32_t *>(sh.srec);
+      const uint32_t np = (n + 1) / 2;  // <= kMaxRec / 2 = 2 * 64 pairs
+      if (lane < np) dst[lane] = src[lane];
+      if (lane + 64 < np) dst[lane + 64] = src[lane + 64];
+    }
+    uint32_t okc = 0;
+    for (int s = 0; s < kRounds; ++s) {
+      if ((uint32_t)s * 64u >= n) break;
+      const uint32_t i = lane + (uint32_t)s * 64u;
+      bool ok = false;
+      if (i < n) {
+        FlowWords f;
+        ok = decode_rec<false>(kp, sh.data, tile_lo, sh.srec[i], f) == NPR_FLOW_OK;
       }
-    } else if (wave == 2) {
-      if (has_prev) {  // fold the group window for wave 1
-        const uint32_t pg = tp / kGroup;
-        uint32_t st = kWinEmpty;
-        Seg c{};
-        if (pg > 0) {
-          const bool inr = (int64_t)pg - 1 - (int64_t)lane >= 0;
-          const LaneSeg L = decode_group_lanes(kp, (int64_t)pg - 1 - lane, inr, win);
-          const int nwin = pg < 64 ? (int)pg : 64;
-          const uint64_t bAnc = __ballot(inr && L.anchor), bPres = __ballot(inr && L.present);
-          const int jp = bAnc ? __builtin_ctzll(bAnc) : nwin;
-          const uint64_t need = jp >= 64 ? ~0ull : ((1ull << jp) - 1ull);
-          st = kWinFail;
-          if (jp < nwin && (bPres & need) == need) {
-            c = fold_window(kp, L, jp);
-            st = kWinAnchored;
-          }
+      okc += (uint32_t)__builtin_popcountll(__ballot(ok));
+    }
+    stamp(kp, t, 3);
+    uint32_t fold = 0xffffffffu;
+    if (lane == 0) {
+      TileSlot *slot = kp.slots + t;
+      const uint32_t ep = kp.epoch;
+      st_agent(&slot->a[0], gran(ep, ex));
+      st_agent(&slot->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
+      st_agent(&slot->a[2], gran(ep, (uint64_t)n | ((uint64_t)okc << 24)));
+      // the previous tile's arrival has returned by now: was it its group's last?
+      if (arrived != 0xffffffffu && arrived == group_size(kp, arrived_g) - 1u) fold = arrived_g;
+      arrived_g = t >> 6;
+      arrived = __hip_atomic_fetch_add(kp.cnt1 + 2 * arrived_g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the chain continues into the next tile unless it ended here (Q3) or nothing was found
+    carry = (entry != kNone && ex >= tile_hi) ? ex : kNone;
+    fold = __builtin_amdgcn_readfirstlane(fold);
+    if (fold != 0xffffffffu) fold_groups(kp, fold);
+    stamp(kp, t, 4);
+    wave_sync();  // done with this tile's LDS before the next commit
+  };
+  for (uint32_t t = c0; t < c1; t += 2) {
+    step(t, qa);
+    if (t + 1 < c1) step(t + 1, qb);
+  }
+  uint32_t fold = 0xffffffffu;
+  if (lane == 0 && arrived == group_size(kp, arrived_g) - 1u) fold = arrived_g;
+  fold = __builtin_amdgcn_readfirstlane(fold);
+  if (fold != 0xffffffffu) fold_groups(kp, fold);
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 2: emit_chunk — ONE WAVE owns the contiguous tiles [c0, c1).
+//   exact prefix before c0 = start ⊕ G2(blocks) ⊕ G1(groups) ⊕ A(tiles): the three 64-wide
+//   windows are loaded together, then folded; a contradiction (a mis-speculated tile m < c0)
+//   is settled by m's exact prefix P(m), published below by m's owner.  Then per tile,
+//   carrying the exact chain position and counts: (tile + 2, its A and its record offsets ->
+//   registers) | the offsets: pass 1's when its entry equals the exact position (the common
+//   case), else a walk | decode every record | record table / status | Ok flows at their
+//   convert_records (reverse-order) positions, ranked by ballot | publish P(t).
+// ---------------------------------------------------------------------------------------------
+struct TileAhead {  // what pass 2 prefetches for a tile
+  u32x4 q[kChunks];
+  uint32_t off0, off1;  // record-offset pairs lane, lane + 64 from the scratch
+  uint64_t a1, a2;      // A granules: entry + 1, n | okc << 24
+};
+
+__device__ __forceinline__ void ahead_issue(const ParseParams &kp, uint32_t t, TileAhead &A) {
+  const uint32_t lane = threadIdx.x & 63u;
+  stage_issue(kp, kp.org + (uint64_t)t * kTile, A.q);
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, kMaxRec * 2, 0x00020000);
+  A.off0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u), 0, 16);  // sc1: L2-served
+  A.off1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u + 256u), 0, 16);
+  A.a1 = ld_agent(&kp.slots[t].a[1]);
+  A.a2 = ld_agent(&kp.slots[t].a[2]);
+}
+
+// exact chain state before tile c: false when a hand-off timed out
+__device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  X = start_seg(kp);
+  const int64_t h = c >> 12, g = c >> 6;
+  if (h > 64) return prefix_generic(kp, X, 0, c, X, t0);  // > 1 GiB before c: the generic walker
+  const int n2 = (int)h, n1 = (int)(g - (h << 6)), n0 = (int)((int64_t)c - (g << 6));
+  // all three windows in flight at once
+  const LaneSeg L2 = load_agg(kp, 2, h - 1 - lane, (int)lane < n2);
+  const LaneSeg L1 = load_agg(kp, 1, g - 1 - lane, (int)lane < n1);
+  const LaneSeg L0 = load_agg(kp, 0, (int64_t)c - 1 - lane, (int)lane < n0);
+  const bool all = __ballot(((int)lane < n2 && !L2.present) || ((int)lane < n1 && !L1.present) ||
+                            ((int)lane < n0 && !L0.present)) == 0ull;
+  Seg y;
+  if (all) {
+    if (n2) X = combine(kp, X, fold_window(kp, L2, n2 - 1));
+    if (n1) X = combine(kp, X, fold_window(kp, L1, n1 - 1));
+    if (n0) X = combine(kp, X, fold_window(kp, L0, n0 - 1));
+  } else {  // not all published yet (fused launch): fold each window as it completes
+    if (n2) {
+      if (!fold_range(kp, 2, 0, n2, y, t0)) return false;
+      X = combine(kp, X, y);
+    }
+    if (n1) {
+      if (!fold_range(kp, 1, h << 6, n1, y, t0)) return false;
+      X = combine(kp, X, y);
+    }
+    if (n0) {
+      if (!fold_range(kp, 0, g << 6, n0, y, t0)) return false;
+      X = combine(kp, X, y);
+    }
+  }
+  if (!X.valid) return prefix_generic(kp, X, 0, c, X, t0);
+  return true;
+}
+
+__device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  TileAhead A, B;  // two tiles in flight (the loop is unrolled by two)
+  ahead_issue(kp, c0, A);
+  if (c0 + 1 < c1) ahead_issue(kp, c0 + 1, B);
+  Seg X;
+  if (!prefix_of(kp, c0, X)) return;
+  uint64_t pos = X.exit, pcnt = X.cnt, pok = X.ok;  // exact chain state entering tile t
+  auto step = [&](uint32_t t, TileAhead &A) {
+    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
+    const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
+    stamp(kp, t, 5);
+    stage_commit(sh.data, A.q);
+    const uint64_t e1 = A.a1 & kMask48, na = A.a2 & 0xffffffull;
+    const bool reuse = tagged(A.a1, kp.epoch) && tagged(A.a2, kp.epoch) && e1 == pos + 1;
+    if (reuse) {  // pass 1 walked this tile from the same (exact) entry: its offsets are the chain's
+      reinterpret_cast<uint32_t *>(sh.srec)[lane] = A.off0;
+      reinterpret_cast<uint32_t *>(sh.srec)[lane + 64] = A.off1;
+    }
+    wave_sync();
+    if (t + 2 < c1) ahead_issue(kp, t + 2, A);
+    uint32_t n = 0;
+    uint64_t ex = pos;
+    if (pos >= tile_lo && pos < tile_hi) {
+      if (reuse) {
+        n = (uint32_t)na;
+        if (n) {  // exit = just past the last record (the walk advances by whole records)
+          const uint32_t rl = sh.srec[n - 1];
+          ex = tile_lo + rl + 16u + hdr(sh.data, rl, 2, kp.big);
         }
-        if (lane == 0) {
-          sh.l2 = c;
-          sh.l2_state = st;
-          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the fold is in LDS before the tag
-          __hip_atomic_store(&sh.l2_tag, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-    } else if (wave == 1) {
-      if (has_prev) {  // resolve tile tp, then write its outputs
-        const uint32_t pi = tp % kGroup;
-        uint32_t s1 = kWinEmpty;
-        Seg l1{};
-        if (pi > 0) {
-          const bool inr = (int)lane < (int)pi;
-          const LaneSeg L = decode_tile_lanes(kp, (int64_t)tp - 1 - lane, inr, win);
-          const uint64_t bAnc = __ballot(inr && L.anchor), bPres = __ballot(inr && L.present);
-          const int jp = bAnc ? __builtin_ctzll(bAnc) : (int)pi;
-          const uint64_t need = (1ull << jp) - 1ull;
-          s1 = kWinFail;
-          if ((bPres & need) == need) {
-            l1 = fold_window(kp, L, jp < (int)pi ? jp : (int)pi - 1);
-            s1 = jp < (int)pi ? (l1.valid ? kWinResolved : kWinFail) : kWinAgg;
-          }
-        }
-        Prefix pre{kp.start, 0, 0};
-        bool ok = true;
-        if (tp != 0) {
-          bool done = false;
-          if (s1 == kWinResolved) {
-            pre = Prefix{l1.exit, l1.cnt, l1.ok};
-            done = true;
-          } else if (s1 == kWinAgg || s1 == kWinEmpty) {
-            while (__hip_atomic_load(&sh.l2_tag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != k)
-              __builtin_amdgcn_s_sleep(1);
-            if (sh.l2_state == kWinAnchored) {
-              const Seg c = s1 == kWinEmpty ? sh.l2 : combine(kp, sh.l2, l1);
-              if (c.valid) {
-                pre = Prefix{c.exit, c.cnt, c.ok};
-                done = true;
-              }
-            }
-          }
-          if (!done) {  // not resolvable from the early words: the blocking look-back
-            Diag dg;
-            ok = lookback(kp, tp, pre, dg);
-          }
-        }
-        const bool slow = ok && tp != 0 && pre.exit != sh.entry[prv];
-        if (lane == 0) {
-          sh.pexit = pre.exit;
-          sh.pcnt = pre.cnt;
-          sh.pok = pre.ok;
-          sh.abort = ok ? 0u : 1u;
-          sh.slow = slow ? 1u : 0u;
-        }
-        if (ok && !slow) {
-          const uint32_t n = sh.n[prv], okc = sh.okc[prv];
-          if (tp != 0 && lane == 0) {
-            TileSlot *slot = kp.slots + tp;
-            st_agent(&slot->p[0], gran(ep, sh.exit[prv]));
-            st_agent(&slot->p[1], gran(ep, pre.cnt + n));
-            st_agent(&slot->p[2], gran(ep, pre.ok + okc));
-          }
-          if (tp == kp.ntiles - 1 && lane == 0) write_summary(kp, pre.cnt + n, pre.ok + okc, sh.exit[prv]);
-          if (kp.stamps && lane == 0) kp.stamps[(uint64_t)tp * 8 + 2] = __builtin_amdgcn_s_memrealtime();
-          if (kp.rec_off || kp.recs || kp.rec_status)
-            write_records(kp, sh.srec[prv], n, ptile_lo, pre.cnt, sh.pstat, lane, 64);
-          if (kp.flows) {
-            for (uint32_t r = lane; r < okc; r += 64) {
-              const uint64_t fi = pre.ok + r;
-              if (fi >= kp.flow_cap) break;
-              const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
-              const u32x4 *src = reinterpret_cast<const u32x4 *>(&sh.park[r * 8]);
-              const u32x4 a0 = src[0], a1 = src[1];
-              u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-              dst[0] = a0;
-              dst[1] = a1;
-              if (kp.flows_v6 && ((a1[2] >> 16) & NPR_FLOW_KIND_IPV6)) {  // IPv6: re-read the addresses
-                const uint64_t p = ((uint64_t)a1[3] << 8) | (a1[2] >> 24);
-                GlobalReader gh{kp.buf + p, kp.len - p};
-                const uint32_t incl = kp.big ? __builtin_bswap32(gh.le32(8)) : gh.le32(8);
-                GlobalReader gr{kp.buf + p + 16, kp.len - p - 16};
-                FlowWords f;
-                decode<true>(gr, incl, f);
-                u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
-                d6[0] = u32x4{f.v6[0], f.v6[1], f.v6[2], f.v6[3]};
-                d6[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
-              }
-            }
-          }
-          if (kp.stamps && lane == 0) kp.stamps[(uint64_t)tp * 8 + 3] = __builtin_amdgcn_s_memrealtime();
-        }
+      } else {
+        ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n);
+        wave_sync();
+        if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
       }
     }
-    __syncthreads();
-    if (sh.abort) return;
+    stamp(kp, t, 6);
 
-    // ---- phase B: decode tile t once, publish its aggregate --------------------------------
-    if (has_cur) {
-      const uint32_t okc = decode_tile(kp, sh, tile_lo, cur, false, 0);
-      if (tid == 0) {
-        sh.okc[cur] = okc;
-        TileSlot *slot = kp.slots + t;
-        if (t == 0 && !(kp.flags & kFlagSpecFirst)) {
-          st_agent(&slot->p[0], gran(ep, sh.exit[cur]));
-          st_agent(&slot->p[1], gran(ep, sh.n[cur]));
-          st_agent(&slot->p[2], gran(ep, okc));
-        } else {
-          st_agent(&slot->a[0], gran(ep, sh.exit[cur]));
-          st_agent(&slot->a[1], gran(ep, sh.entry[cur] == kNone ? 0ull : sh.entry[cur] + 1));
-          st_agent(&slot->a[2], gran(ep, (uint64_t)sh.n[cur] | ((uint64_t)okc << 24)));
-        }
-        if (kp.stamps) kp.stamps[(uint64_t)t * 8 + 1] = __builtin_amdgcn_s_memrealtime();
-      }
-    }
-
-    // ---- slow path: tile tp speculated wrong -> reload it, redo from the exact entry --------
-    if (sh.slow) {
-      __syncthreads();  // everyone is done with tile t's data
-      u32x4 r2[kPrefetch];
-      prefetch_tile(kp, tp, r2);
-      commit_tile(sh.data, r2);
-      __syncthreads();
-      const uint64_t ptile_hi = ptile_lo + kTile < kp.len ? ptile_lo + kTile : kp.len;
-      const uint64_t e = sh.pexit;
-      if (wave == 0) {
-        uint32_t n = 0;
-        uint64_t ex = e;
-        if (e >= ptile_lo && e < ptile_hi) ex = walk_tile(kp, sh.data, sh.srec[prv], ptile_lo, ptile_hi, e, n);
-        if (lane == 0) {
-          sh.n[prv] = n;
-          sh.exit[prv] = ex;
+    // ---- decode, record table, Ok flows at reverse positions (rank = ballot prefix)
+    uint32_t okbase = 0;
+    for (int s = 0; s < kRounds; ++s) {
+      if ((uint32_t)s * 64u >= n) break;
+      const uint32_t i = lane + (uint32_t)s * 64u;
+      FlowWords f;
+      bool ok = false;
+      uint32_t rel = 0;
+      if (i < n) {
+        rel = sh.srec[i];
+        const uint64_t p = tile_lo + rel;
+        const uint32_t st = decode_rec<true>(kp, sh.data, tile_lo, rel, f);
+        ok = st == NPR_FLOW_OK;
+        const uint64_t idx = pcnt + i;
+        if (idx < kp.rec_cap) {
+          if (kp.rec_status) kp.rec_status[idx] = (uint8_t)st;
+          if (kp.rec_off) kp.rec_off[idx] = p;
+          if (kp.recs) {
+            const bool big = kp.big;
+            uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
+            row[0] = p;
+            row[1] = (uint64_t)hdr(sh.data, rel, 0, big) | ((uint64_t)hdr(sh.data, rel, 1, big) << 32);
+            row[2] = (uint64_t)hdr(sh.data, rel, 2, big) | ((uint64_t)hdr(sh.data, rel, 3, big) << 32);
+          }
         }
       }
-      __syncthreads();
-      const uint32_t n = sh.n[prv];
-      if (kp.rec_off || kp.recs)
-        write_records(kp, sh.srec[prv], n, ptile_lo, sh.pcnt, nullptr, tid, kBlock);
-      ParseParams kq = kp;
-      kq.pcnt_slow = sh.pcnt;
-      const uint32_t okc = decode_tile(kq, sh, ptile_lo, prv, true, sh.pok);
-      if (tid == 0) {
-        TileSlot *slot = kp.slots + tp;
-        st_agent(&slot->p[0], gran(ep, sh.exit[prv]));
-        st_agent(&slot->p[1], gran(ep, sh.pcnt + n));
-        st_agent(&slot->p[2], gran(ep, sh.pok + okc));
-        if (tp == kp.ntiles - 1) write_summary(kp, sh.pcnt + n, sh.pok + okc, sh.exit[prv]);
-        sh.slow = 0;
+      const uint64_t bal = __ballot(ok);
+      if (ok && kp.flows) {
+        const uint64_t fi = pok + okbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        if (fi < kp.flow_cap) {
+          const uint64_t p = tile_lo + rel;
+          const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
+          u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
+          dst[0] = u32x4{f.d[0], f.d[1], f.d[2], f.d[3]};
+          dst[1] = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+          if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) {
+            u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
+            d6[0] = u32x4{f.v6[0], f.v6[1], f.v6[2], f.v6[3]};
+            d6[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
+          }
+        }
+      }
+      okbase += (uint32_t)__builtin_popcountll(bal);
+    }
+    pos = ex;
+    pcnt += n;
+    pok += okbase;
+    if (lane == 0) {
+      const uint32_t ep = kp.epoch;
+      TileSlot *slot = kp.slots + t;
+      st_agent(&slot->p[0], gran(ep, pos));
+      st_agent(&slot->p[1], gran(ep, pcnt));
+      st_agent(&slot->p[2], gran(ep, pok));
+      if (t == kp.ntiles - 1) {
+        uint32_t fl = 0;
+        if ((kp.rec_off || kp.recs || kp.rec_status) && pcnt > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
+        if (kp.flows && pok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
+        kp.summary->n_records = pcnt;
+        kp.summary->n_flows = pok;
+        kp.summary->consumed = pos;
+        kp.summary->flags = fl;
+        kp.summary->epoch = kp.epoch;
       }
     }
-
-    // (6) tile t+G: registers -> LDS (every wave is done with the buffer)
-    __syncthreads();
-    if (has_next) commit_tile(sh.data, q);
-    // group aggregate of t's group (its last tile), for the next iteration's resolvers
-    if (has_cur && t % kGroup == kGroup - 1 && wave == 3) {
-      if (!publish_group(kp, t / kGroup) && lane == 0) sh.abort = 1u;
-    }
-    __syncthreads();
-    if (sh.abort) return;
+    stamp(kp, t, 7);
+    wave_sync();  // done with this tile's LDS before the next commit
+  };
+  for (uint32_t t = c0; t < c1; t += 2) {
+    step(t, A);
+    if (t + 1 < c1) step(t + 1, B);
   }
 }
 
-hipError_t launch_parse_pipe(const ParseParams &p, uint32_t grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse_pipe, dim3(grid), dim3(kBlock), 0, s, p);
-  return hipGetLastError();
+// pass 1 alone / pass 2 alone (two launches; diagnostics) and both fused in one persistent grid:
+// a wave moves from its scan chunk straight to its emit chunk, whose prefix fold waits only for
+// the aggregates of earlier chunks (lower, earlier-dispatched workgroups: no deadlock).
+__global__ __launch_bounds__(kWave) void k_scan_tiles(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ParseShared sh;
+  uint32_t c0, c1;
+  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
+  if (c0 < c1) scan_chunk(kp, sh, c0, c1);
+}
+__global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ParseShared sh;
+  uint32_t c0, c1;
+  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
+  if (c0 < c1) emit_chunk(kp, sh, c0, c1);
+}
+__global__ __launch_bounds__(kWave) void k_parse_fused(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ParseShared sh;
+  uint32_t c0, c1;
+  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
+  if (c0 >= c1) return;
+  scan_chunk(kp, sh, c0, c1);
+  emit_chunk(kp, sh, c0, c1);
 }
 
-int pipe_blocks_per_cu() {
+static int per_cu(const void *k) {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_parse_pipe, kBlock, 0) != hipSuccess) return 1;
-  return n;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWave, 0) != hipSuccess) return 1;
+  return n > 0 ? n : 1;
+}
+int scan_blocks_per_cu() { return per_cu((const void *)k_scan_tiles); }
+int emit_blocks_per_cu() { return per_cu((const void *)k_emit_tiles); }
+int fused_blocks_per_cu() { return per_cu((const void *)k_parse_fused); }
+
+hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
+  const uint32_t g1 = grid_scan < p.ntiles ? grid_scan : p.ntiles;
+  if (grid_emit == 0) {  // fused
+    hipLaunchKernelGGL(k_parse_fused, dim3(g1), dim3(kWave), 0, s, p);
+    return hipGetLastError();
+  }
+  const uint32_t g2 = grid_emit < p.ntiles ? grid_emit : p.ntiles;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(g1), dim3(kWave), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_emit_tiles, dim3(g2), dim3(kWave), 0, s, p);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,12 +1,15 @@
 #!/bin/bash
-# Parity tests + bench of both kernel variants (+ stamps of the default one).
+# Parity tests + bench (fused default; stamps run of the fused and the two-launch variants).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out
 TAG="${1:-q}"
 run() { local lim=$1 log=$2; shift 2; timeout -k 10 "$lim" "$@" > "$R/gpurun_out/$log" 2>&1; local rc=$?
         echo "[$(date +%T)] $* -> rc=$rc" | tee -a "$R/gpurun_out/steps.log"; return $rc; }
 run 900 "gpu_tests_$TAG.log" python -m pytest tests -m gpu -q -x -p no:cacheprovider
-rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-run 300 "bench_${TAG}_pipe.log" python bench.py --steps 50 --warmup 10 --no-cpu --stats || exit $?
-NPR_KERNEL=tile run 300 "bench_${TAG}_tile.log" python bench.py --steps 50 --warmup 10 --no-cpu || exit $?
-exit $rc
+rc=$?; [ $rc -eq 0 ] || exit $rc   # any failure may be a device fault: run nothing more
+run 300 "bench_${TAG}.log" python bench.py --steps 50 --warmup 10 --no-cpu || exit $?
+run 300 "bench_${TAG}_stats.log" python bench.py --steps 20 --warmup 5 --no-cpu --stats || exit $?
+cp gpurun_out/stamps_rank0.npy gpurun_out/stamps_${TAG}_fused.npy
+NPR_FUSED=0 run 300 "bench_${TAG}_2k.log" python bench.py --steps 50 --warmup 10 --no-cpu --stats || exit $?
+cp gpurun_out/stamps_rank0.npy gpurun_out/stamps_${TAG}_2k.npy
+exit 0

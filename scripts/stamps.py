@@ -4,30 +4,17 @@ import sys
 import numpy as np
 
 s = np.load(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/stamps_rank0.npy").astype(np.int64)
-if len(sys.argv) > 2 and sys.argv[2] == "pipe":  # [0] iter start [1] decoded [2] resolved [3] written
-    t0 = s[:, 0].min()
-    st = (s[:, :4] - t0) / 100.0
-    print("tiles", len(st), "span us %.2f" % st[:, 3].max())
-    for i, nm in enumerate(["phase1", "until resolved", "outputs"]):
-        d = st[:, i + 1] - st[:, i]
-        print(f"{nm:15s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
-    sp = (s[:, 4] - s[:, 0]) / 100.0
-    wk = (s[:, 5] - s[:, 4]) / 100.0
-    dc = (s[:, 1] - s[:, 5]) / 100.0
-    for nm, d in (("  spec", sp), ("  walk", wk), ("  decode+park", dc)):
-        print(f"{nm:15s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
-    for q in np.linspace(0, len(st) - 1, 9).astype(int):
-        print(q, "start %.2f decoded %.2f resolved %.2f written %.2f" % tuple(st[q]))
-    sys.exit(0)
+# two-pass layout: [0] scan tile start [1] entry known [2] walked [3] counted [4] published (+group folds)
+#                  [5] emit tile start [6] walked [7] written
 t0 = s[:, 0].min()
-st = (s[:, :6] - t0) / 100.0  # us (s_memrealtime = 100 MHz)
-print("tiles", len(st), "span us %.2f" % st[:, 5].max())
-ph = np.diff(st, axis=1)
-for i, nm in enumerate(["stage", "spec", "walk+count", "lookback", "output"]):
-    print(f"{nm:12s} mean {ph[:, i].mean():6.2f} med {np.median(ph[:, i]):6.2f} p90 {np.percentile(ph[:, i], 90):6.2f}"
-          f" max {ph[:, i].max():6.2f}")
-print("life mean %.2f" % (st[:, 5] - st[:, 0]).mean(), " spins/tile %.2f" % (s[:, 7] & 0xFFFFF).mean())
-for q in np.linspace(0, len(st) - 1, 9).astype(int):
-    print(q, "start %.2f staged %.2f spec %.2f counted %.2f prefix %.2f end %.2f" % tuple(st[q]))
-ts = np.arange(0, st[:, 5].max(), max(st[:, 5].max() / 30, 0.5))
-print("active", [int(((st[:, 0] <= x) & (st[:, 5] > x)).sum()) for x in ts])
+us = (s - t0) / 100.0  # s_memrealtime = 100 MHz
+print("tiles", len(s), "scan span us %.2f" % (us[:, 4].max() - us[:, 0].min()),
+      "emit span us %.2f" % (us[:, 7].max() - us[:, 5].min()), "gap us %.2f" % (us[:, 5].min() - us[:, 4].max()))
+for a, b, nm in ((0, 1, "entry"), (1, 2, "walk"), (2, 3, "count"), (3, 4, "pub+fold"), (5, 6, "walk"),
+                 (6, 7, "decode+write"), (0, 4, "scan tile"), (5, 7, "emit tile")):
+    d = us[:, b] - us[:, a]
+    print(f"{nm:14s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+for c, nm in ((0, "scan"), (5, "emit")):
+    e = c + 2 if c == 5 else 4
+    ts = np.linspace(us[:, c].min(), us[:, e].max(), 12)
+    print(nm, "active", [int(((us[:, c] <= x) & (us[:, e] > x)).sum()) for x in ts])
