@@ -34,10 +34,12 @@ struct npr_ctx {
   int stats_mode = 0;               // 2 = also per-tile phase stamps
   DevBuf stamps;
   uint64_t stamp_tiles = 0;
-  DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
+  DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile (full mode)
+  DevBuf park, park_v6;    // pass-1 parked flows: kMaxOk 32-B rows per tile (light mode)
   DevBuf counters;         // arrival counters: cnt1[g] at word 2g, cnt2[h] at word 2h+1 (layout independent of the input)
   bool dirty = false;
-  uint32_t grid_scan = 0, grid_emit = 0;  // persistent grids: CUs x resident workgroups per CU      // a launch timed out: counters may be non-zero -> clear before the next launch
+  uint32_t grid_scan = 0, grid_emit = 0;  // persistent grids: CUs x resident workgroups per CU
+  bool light = false;                     // flows-only launches park flows in pass 1 (NPR_LIGHT=1)      // a launch timed out: counters may be non-zero -> clear before the next launch
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -124,7 +126,8 @@ static uint64_t counter_bytes(uint64_t nt) { return (2 * ngroups1(nt) + 2) * siz
 
 uint64_t npr_workspace_bytes(uint64_t len) {
   const uint64_t nt = tiles_for(len, 0, nullptr);
-  return slot_bytes(nt) + counter_bytes(nt) + nt * npr::kMaxRec * sizeof(uint16_t);
+  // + the larger of the full-mode offset scratch and the light-mode parked flows (+ IPv6 rows)
+  return slot_bytes(nt) + counter_bytes(nt) + nt * std::max<uint64_t>(npr::kMaxRec * sizeof(uint16_t), 2 * npr::kMaxOk * 32);
 }
 
 npr_status npr_ctx_create(int device, npr_ctx **out) {
@@ -146,9 +149,11 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
-  // NPR_FUSED=0 selects the two-launch variant (per-pass profiling); NPR_*_PER_CU override occupancy
+  // NPR_FUSED=1 selects the one-launch variant; NPR_*_PER_CU override occupancy
   const char *fz = getenv("NPR_FUSED");
-  const bool fused = !(fz && strcmp(fz, "0") == 0);
+  const bool fused = fz && strcmp(fz, "1") == 0;  // two launches unless NPR_FUSED=1 (measured faster)
+  const char *lt = getenv("NPR_LIGHT");
+  c->light = lt && strcmp(lt, "1") == 0;
   int per_cu_scan = fused ? npr::fused_blocks_per_cu() : npr::scan_blocks_per_cu();
   int per_cu_emit = fused ? 0 : npr::emit_blocks_per_cu();
   if (const char *v = getenv("NPR_SCAN_PER_CU")) per_cu_scan = std::max(1, atoi(v));
@@ -163,7 +168,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->slots, &c->srec, &c->counters, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+  for (DevBuf *b : {&c->slots, &c->srec, &c->park, &c->park_v6, &c->counters, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->scratch})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
@@ -263,7 +268,14 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
   if ((st = ensure(c, c->counters, counter_bytes(nt), true))) return st;
-  if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
+  // light mode (flows only, opt-in with NPR_LIGHT=1): pass 1 parks the flows, pass 2 copies them
+  const bool light = c->light && !o->record_offsets && !o->records && !o->record_status;
+  if (light) {
+    if ((st = ensure(c, c->park, nt * npr::kMaxOk * 32, false))) return st;
+    if (o->flows_v6 && (st = ensure(c, c->park_v6, nt * npr::kMaxOk * 32, false))) return st;
+  } else if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) {
+    return st;
+  }
   hipStream_t s = pick(c, stream);
   if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
     c->epoch = 1;
@@ -292,7 +304,10 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   p.groups2 = p.groups1 + p.ngroups1;
   p.cnt1 = (uint32_t *)c->counters.p;      // word 2g
   p.cnt2 = (uint32_t *)c->counters.p + 1;  // word 2h + 1
-  p.srec_g = (uint16_t *)c->srec.p;
+  p.srec_g = light ? nullptr : (uint16_t *)c->srec.p;
+  p.park = light ? (uint32_t *)c->park.p : nullptr;
+  p.park_v6 = light && o->flows_v6 ? (uint32_t *)c->park_v6.p : nullptr;
+  if (light) p.flags |= npr::kFlagLight;
   p.abort_word = c->abort_word;
   p.rec_off = o->record_offsets;
   p.recs = o->records;

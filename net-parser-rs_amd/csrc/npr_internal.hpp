@@ -12,11 +12,17 @@ namespace npr {
 // Tile geometry of the parse+extract kernels: ONE WAVE per tile.
 constexpr int kBlock = 256;            // workgroup size of the auxiliary kernels (dense extract, compaction)
 constexpr int kWave = 64;              // the parse kernels: one-wave workgroups
-constexpr int kTile = 4096;            // bytes of the record stream owned by one tile
+#ifndef NPR_TILE_BYTES
+#define NPR_TILE_BYTES 4096
+#endif
+constexpr int kTile = NPR_TILE_BYTES;  // bytes of the record stream owned by one tile (one wave)
 constexpr int kHalo = 128;             // bytes staged past the tile (headers + fast-decode window of straddlers)
 constexpr int kStage = kTile + kHalo;  // bytes staged in LDS per tile
 constexpr int kMaxRec = kTile / 16;    // every record is >= 16 B
 constexpr int kRounds = kMaxRec / kWave;  // decode rounds of 64 records
+// An Ok record spans >= 16 + 42 bytes (header + Ethernet/IPv4/UDP), so at most this many Ok
+// records start in one tile: the per-tile capacity of the parked-flow scratch.
+constexpr int kMaxOk = (kTile + 57) / 58 + 1;
 
 // Per-tile hand-off slot: A = speculative aggregate (k_scan_tiles), P = exact inclusive prefix
 // (k_emit_tiles).  Each word is an 8-byte {tag:16 | value:48} granule written by ONE
@@ -34,6 +40,7 @@ struct alignas(32) GroupSlot {
 
 enum : uint32_t {
   kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
+  kFlagLight = 4u,        // flows only (no record table / status): pass 1 parks the flows, pass 2 copies
 };
 
 // optional diagnostic counters (ParseParams::stats, NULL in production launches)
@@ -62,6 +69,8 @@ struct ParseParams {
   uint32_t *cnt1, *cnt2;   // arrival counters (zero between launches)
   uint32_t ngroups1, ngroups2;
   uint16_t *srec_g;        // pass-1 record offsets, kMaxRec per tile (pass 2 reuses them)
+  uint32_t *park;          // light mode: pass-1 Ok flows, kMaxOk 32-B rows per tile
+  uint32_t *park_v6;       // light mode: their IPv6 addresses (when flows_v6)
   uint32_t *abort_word;    // == epoch once any tile aborted
   uint64_t *rec_off;
   npr_record *recs;

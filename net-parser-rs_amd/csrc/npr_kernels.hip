@@ -347,6 +347,11 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// a value every lane holds identically, made visibly wave-uniform (scalar registers)
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
+
 // A segment of consecutive tiles [first, last] under speculation.
 struct Seg {
   uint64_t entry, exit, cnt, ok;
@@ -622,11 +627,12 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
   const uint32_t span = (uint32_t)(tile_hi - tile_lo);
   const uint64_t av = kp.len - tile_lo;
   const uint32_t avail = av > 0xffffffffull ? 0xffffffffu : (uint32_t)av;  // bytes from tile_lo
-  uint64_t p = entry;
+  uint64_t p = uni64(entry);
   uint32_t n = 0;
   while (p < tile_hi) {
     const uint32_t r = (uint32_t)(p - tile_lo);
-    const uint32_t incl = hdr(w, r, 2, big);
+    // wave-uniform (one address): readfirstlane keeps the chain position scalar
+    const uint32_t incl = __builtin_amdgcn_readfirstlane(hdr(w, r, 2, big));
     if (kp.len - p < 16 || kp.len - p - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
     if (incl > (uint32_t)kTile) {  // a record longer than a tile: no stride to speculate on
       if (lane == 0) srec[n] = (uint16_t)r;
@@ -661,8 +667,10 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
   return p;
 }
 
+// diagnostics (DIAG kernel variants only: the production kernels carry none of this)
+template <bool DIAG>
 __device__ __forceinline__ void stamp(const ParseParams &kp, uint32_t t, int k) {
-  if (kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * 8 + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 // LDS written by some lanes of this wave, then read by others: LDS executes one wave's requests
@@ -711,7 +719,8 @@ __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
   sc.has_ref = kp.len >= kp.start + 16;
   GlobalReader gr{kp.buf + kp.start, sc.has_ref ? 4ull : 0ull};
   const uint32_t v = gr.le32(0);
-  sc.ts_ref = kp.big ? __builtin_bswap32(v) : v;
+  sc.ts_ref = __builtin_amdgcn_readfirstlane(kp.big ? __builtin_bswap32(v) : v);
+  sc.frac_max = __builtin_amdgcn_readfirstlane(sc.frac_max);
   sc.avail = 0;
   sc.exact_end = true;
   return sc;
@@ -734,6 +743,18 @@ __device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t 
     if (weak == 0xffffffffu && b1) weak = base + (uint32_t)__builtin_ctzll(b1);
   }
   return weak == 0xffffffffu ? kNone : tile_lo + weak;
+}
+
+// one npr_flow row (8 words) / its IPv6 side row, 16-B stores
+__device__ __forceinline__ void put_flow(uint32_t *row, const FlowWords &f, uint64_t p) {
+  u32x4 *d = reinterpret_cast<u32x4 *>(row);
+  d[0] = u32x4{f.d[0], f.d[1], f.d[2], f.d[3]};
+  d[1] = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+}
+__device__ __forceinline__ void put_v6(uint32_t *row, const FlowWords &f) {
+  u32x4 *d = reinterpret_cast<u32x4 *>(row);
+  d[0] = u32x4{f.v6[0], f.v6[1], f.v6[2], f.v6[3]};
+  d[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
 }
 
 struct ParseShared {  // one wave's LDS
@@ -789,6 +810,7 @@ __device__ __forceinline__ void fold_groups(const ParseParams &kp, uint32_t g) {
 // returned value is consumed one tile later (its round trip overlaps the next tile): the last
 // arriver of a 64-tile group folds G1, the last group of a 4096-tile block folds G2.
 // ---------------------------------------------------------------------------------------------
+template <bool DIAG, bool LIGHT>
 __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
   const uint32_t lane = threadIdx.x & 63u;
   // two tiles in flight: register sets qa / qb alternate (the loop is unrolled by two so the
@@ -802,7 +824,7 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
   auto step = [&](uint32_t t, u32x4 (&q)[kChunks]) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
-    stamp(kp, t, 0);
+    stamp<DIAG>(kp, t, 0);
     stage_commit(sh.data, q);
     wave_sync();
     if (t + 2 < c1) stage_issue(kp, tile_lo + 2ull * kTile, q);
@@ -812,17 +834,20 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       entry = kp.start;
     } else if (carry == kNone) {
       entry = speculate(sc, kp, sh.data, tile_lo, (uint32_t)(tile_hi - tile_lo));
-      if (kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
+      if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
     }
-    stamp(kp, t, 1);
+    stamp<DIAG>(kp, t, 1);
+    entry = uni64(entry);
     uint32_t n = 0;
     uint64_t ex = entry == kNone ? 0ull : entry;
     if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, entry, n);
+    ex = uni64(ex);
     wave_sync();
-    stamp(kp, t, 2);
+    stamp<DIAG>(kp, t, 2);
 
-    // ---- offsets -> scratch (pairs of u16); Ok count (status-only decode)
-    if (kp.srec_g) {
+    // ---- full mode: offsets -> scratch (pairs of u16) + Ok count (status-only decode);
+    //      light mode: decode with fields, Ok flows parked in tile order
+    if (!LIGHT && kp.srec_g) {
       uint32_t *dst = reinterpret_cast<uint32_t *>(kp.srec_g + (uint64_t)t * kMaxRec);
       const uint32_t *src = reinterpret_cast<const uint32_t *>(sh.srec);
       const uint32_t np = (n + 1) / 2;  // <= kMaxRec / 2 = 2 * 64 pairs
@@ -834,13 +859,24 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       if ((uint32_t)s * 64u >= n) break;
       const uint32_t i = lane + (uint32_t)s * 64u;
       bool ok = false;
+      FlowWords f;
+      uint32_t rel = 0;
       if (i < n) {
-        FlowWords f;
-        ok = decode_rec<false>(kp, sh.data, tile_lo, sh.srec[i], f) == NPR_FLOW_OK;
+        rel = sh.srec[i];
+        ok = decode_rec<LIGHT>(kp, sh.data, tile_lo, rel, f) == NPR_FLOW_OK;
       }
-      okc += (uint32_t)__builtin_popcountll(__ballot(ok));
+      const uint64_t bal = __ballot(ok);
+      if (LIGHT && ok) {
+        const uint32_t r = okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        if (r < (uint32_t)kMaxOk) {  // always: see kMaxOk
+          const uint64_t row = ((uint64_t)t * kMaxOk + r) * 8;
+          put_flow(kp.park + row, f, tile_lo + rel);
+          if (kp.park_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.park_v6 + row, f);
+        }
+      }
+      okc += (uint32_t)__builtin_popcountll(bal);
     }
-    stamp(kp, t, 3);
+    stamp<DIAG>(kp, t, 3);
     uint32_t fold = 0xffffffffu;
     if (lane == 0) {
       TileSlot *slot = kp.slots + t;
@@ -854,10 +890,10 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       arrived = __hip_atomic_fetch_add(kp.cnt1 + 2 * arrived_g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // the chain continues into the next tile unless it ended here (Q3) or nothing was found
-    carry = (entry != kNone && ex >= tile_hi) ? ex : kNone;
+    carry = uni64((entry != kNone && ex >= tile_hi) ? ex : kNone);
     fold = __builtin_amdgcn_readfirstlane(fold);
     if (fold != 0xffffffffu) fold_groups(kp, fold);
-    stamp(kp, t, 4);
+    stamp<DIAG>(kp, t, 4);
     wave_sync();  // done with this tile's LDS before the next commit
   };
   for (uint32_t t = c0; t < c1; t += 2) {
@@ -934,6 +970,7 @@ __device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X) {
   return true;
 }
 
+template <bool DIAG>
 __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
   const uint32_t lane = threadIdx.x & 63u;
   TileAhead A, B;  // two tiles in flight (the loop is unrolled by two)
@@ -941,14 +978,15 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
   if (c0 + 1 < c1) ahead_issue(kp, c0 + 1, B);
   Seg X;
   if (!prefix_of(kp, c0, X)) return;
-  uint64_t pos = X.exit, pcnt = X.cnt, pok = X.ok;  // exact chain state entering tile t
+  uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
   auto step = [&](uint32_t t, TileAhead &A) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
-    stamp(kp, t, 5);
+    stamp<DIAG>(kp, t, 5);
     stage_commit(sh.data, A.q);
-    const uint64_t e1 = A.a1 & kMask48, na = A.a2 & 0xffffffull;
-    const bool reuse = tagged(A.a1, kp.epoch) && tagged(A.a2, kp.epoch) && e1 == pos + 1;
+    const uint64_t a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: wave-uniform
+    const uint64_t e1 = a1 & kMask48, na = a2 & 0xffffffull;
+    const bool reuse = tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && e1 == pos + 1;
     if (reuse) {  // pass 1 walked this tile from the same (exact) entry: its offsets are the chain's
       reinterpret_cast<uint32_t *>(sh.srec)[lane] = A.off0;
       reinterpret_cast<uint32_t *>(sh.srec)[lane + 64] = A.off1;
@@ -961,16 +999,16 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
       if (reuse) {
         n = (uint32_t)na;
         if (n) {  // exit = just past the last record (the walk advances by whole records)
-          const uint32_t rl = sh.srec[n - 1];
-          ex = tile_lo + rl + 16u + hdr(sh.data, rl, 2, kp.big);
+          const uint32_t rl = __builtin_amdgcn_readfirstlane(sh.srec[n - 1]);
+          ex = tile_lo + rl + 16u + __builtin_amdgcn_readfirstlane(hdr(sh.data, rl, 2, kp.big));
         }
       } else {
         ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n);
         wave_sync();
-        if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
+        if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
       }
     }
-    stamp(kp, t, 6);
+    stamp<DIAG>(kp, t, 6);
 
     // ---- decode, record table, Ok flows at reverse positions (rank = ballot prefix)
     uint32_t okbase = 0;
@@ -1016,7 +1054,7 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
       }
       okbase += (uint32_t)__builtin_popcountll(bal);
     }
-    pos = ex;
+    pos = uni64(ex);
     pcnt += n;
     pok += okbase;
     if (lane == 0) {
@@ -1036,8 +1074,154 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
         kp.summary->epoch = kp.epoch;
       }
     }
-    stamp(kp, t, 7);
+    stamp<DIAG>(kp, t, 7);
     wave_sync();  // done with this tile's LDS before the next commit
+  };
+  for (uint32_t t = c0; t < c1; t += 2) {
+    step(t, A);
+    if (t + 1 < c1) step(t + 1, B);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// pass 2, light mode (flows only): emit_light_chunk — ONE WAVE owns the tiles [c0, c1).
+//   Same exact prefix as emit_chunk; then per tile, when pass 1 started the tile at the exact
+//   chain position (the common case), its parked Ok flows are simply copied to their
+//   convert_records positions — no staging, no walk, no decode.  A tile pass 1 mis-speculated
+//   is staged, walked from the exact position and decoded here (the full path).
+// ---------------------------------------------------------------------------------------------
+struct ParkAhead {  // what light pass 2 prefetches for a tile
+  u32x4 r0, r1;     // parked flow row `lane`
+  u32x4 v0, v1;     // its IPv6 side row (when flows_v6)
+  uint64_t a0, a1, a2;
+};
+
+__device__ __forceinline__ void park_issue(const ParseParams &kp, uint32_t t, ParkAhead &P) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t row = (uint64_t)t * kMaxOk * 8;
+  // sc1 (aux 16): L2-served, never a stale L1 line from an earlier launch
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park + row), 0, kMaxOk * 32, 0x00020000);
+  P.r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 32u), 0, 16);
+  P.r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 32u + 16u), 0, 16);
+  if (kp.flows_v6) {
+    const __amdgpu_buffer_rsrc_t r6 =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park_v6 + row), 0, kMaxOk * 32, 0x00020000);
+    P.v0 = __builtin_amdgcn_raw_buffer_load_b128(r6, (int)(lane * 32u), 0, 16);
+    P.v1 = __builtin_amdgcn_raw_buffer_load_b128(r6, (int)(lane * 32u + 16u), 0, 16);
+  }
+  P.a0 = ld_agent(&kp.slots[t].a[0]);
+  P.a1 = ld_agent(&kp.slots[t].a[1]);
+  P.a2 = ld_agent(&kp.slots[t].a[2]);
+}
+
+template <bool DIAG>
+__device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
+  const uint32_t lane = threadIdx.x & 63u;
+  ParkAhead A, B;  // two tiles in flight (the loop is unrolled by two)
+  park_issue(kp, c0, A);
+  if (c0 + 1 < c1) park_issue(kp, c0 + 1, B);
+  Seg X;
+  if (!prefix_of(kp, c0, X)) return;
+  uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
+  auto step = [&](uint32_t t, ParkAhead &A) {
+    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
+    const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
+    stamp<DIAG>(kp, t, 5);
+    const uint64_t a0 = rl64(A.a0, 0), a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: uniform
+    const uint32_t ep = kp.epoch;
+    const bool reuse = tagged(a0, ep) && tagged(a1, ep) && tagged(a2, ep) && (a1 & kMask48) == pos + 1;
+    uint32_t n = 0, okc = 0;
+    uint64_t ex = pos;
+    if (pos >= tile_lo && pos < tile_hi) {
+      if (reuse) {
+        n = (uint32_t)(a2 & 0xffffffull);
+        okc = (uint32_t)((a2 >> 24) & 0xffffffull);
+        ex = a0 & kMask48;
+        stamp<DIAG>(kp, t, 6);
+        if (kp.flows) {
+          if (lane < okc && pok + lane < kp.flow_cap) {
+            const uint64_t o = kp.flow_cap - 1 - (pok + lane);  // convert_records pops from the end
+            u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
+            d[0] = A.r0;
+            d[1] = A.r1;
+            if (kp.flows_v6 && ((A.r1[2] >> 16) & NPR_FLOW_KIND_IPV6)) {
+              u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
+              d6[0] = A.v0;
+              d6[1] = A.v1;
+            }
+          }
+          if (okc > 64u) {  // rows 64.. (tiles of many small Ok records): straight copies
+            const uint32_t r = 64u + lane;
+            if (r < okc && pok + r < kp.flow_cap) {
+              const uint64_t src = ((uint64_t)t * kMaxOk + r) * 8;
+              const uint64_t o = kp.flow_cap - 1 - (pok + r);
+              const u32x4 *s = reinterpret_cast<const u32x4 *>(kp.park + src);
+              u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
+              const u32x4 x0 = __builtin_nontemporal_load(s), x1 = __builtin_nontemporal_load(s + 1);
+              d[0] = x0;
+              d[1] = x1;
+              if (kp.flows_v6 && ((x1[2] >> 16) & NPR_FLOW_KIND_IPV6)) {
+                const u32x4 *s6 = reinterpret_cast<const u32x4 *>(kp.park_v6 + src);
+                u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
+                d6[0] = __builtin_nontemporal_load(s6);
+                d6[1] = __builtin_nontemporal_load(s6 + 1);
+              }
+            }
+          }
+        }
+      } else {  // pass 1 started this tile elsewhere: stage, walk from the exact position, decode
+        if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
+        u32x4 q[kChunks];
+        stage_issue(kp, tile_lo, q);
+        stage_commit(sh.data, q);
+        wave_sync();
+        ex = uni64(walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n));
+        wave_sync();
+        stamp<DIAG>(kp, t, 6);
+        for (int s = 0; s < kRounds; ++s) {
+          if ((uint32_t)s * 64u >= n) break;
+          const uint32_t i = lane + (uint32_t)s * 64u;
+          FlowWords f;
+          bool ok = false;
+          uint32_t rel = 0;
+          if (i < n) {
+            rel = sh.srec[i];
+            ok = decode_rec<true>(kp, sh.data, tile_lo, rel, f) == NPR_FLOW_OK;
+          }
+          const uint64_t bal = __ballot(ok);
+          if (ok && kp.flows) {
+            const uint64_t fi = pok + okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+            if (fi < kp.flow_cap) {
+              const uint64_t o = kp.flow_cap - 1 - fi;
+              put_flow(kp.flows + o * 8, f, tile_lo + rel);
+              if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.flows_v6 + o * 8, f);
+            }
+          }
+          okc += (uint32_t)__builtin_popcountll(bal);
+        }
+        wave_sync();  // done with the staged tile
+      }
+    }
+    if (t + 2 < c1) park_issue(kp, t + 2, A);
+    pos = uni64(ex);
+    pcnt += n;
+    pok += okc;
+    if (lane == 0) {
+      TileSlot *slot = kp.slots + t;
+      st_agent(&slot->p[0], gran(ep, pos));
+      st_agent(&slot->p[1], gran(ep, pcnt));
+      st_agent(&slot->p[2], gran(ep, pok));
+      if (t == kp.ntiles - 1) {
+        uint32_t fl = 0;
+        if (kp.flows && pok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
+        kp.summary->n_records = pcnt;
+        kp.summary->n_flows = pok;
+        kp.summary->consumed = pos;
+        kp.summary->flags = fl;
+        kp.summary->epoch = kp.epoch;
+      }
+    }
+    stamp<DIAG>(kp, t, 7);
   };
   for (uint32_t t = c0; t < c1; t += 2) {
     step(t, A);
@@ -1048,25 +1232,31 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
 // pass 1 alone / pass 2 alone (two launches; diagnostics) and both fused in one persistent grid:
 // a wave moves from its scan chunk straight to its emit chunk, whose prefix fold waits only for
 // the aggregates of earlier chunks (lower, earlier-dispatched workgroups: no deadlock).
+template <bool DIAG, bool LIGHT>
 __global__ __launch_bounds__(kWave) void k_scan_tiles(ParseParams kp) {
   __shared__ __attribute__((aligned(16))) ParseShared sh;
   uint32_t c0, c1;
   chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
-  if (c0 < c1) scan_chunk(kp, sh, c0, c1);
+  if (c0 < c1) scan_chunk<DIAG, LIGHT>(kp, sh, c0, c1);
 }
+template <bool DIAG, bool LIGHT>
 __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
   __shared__ __attribute__((aligned(16))) ParseShared sh;
   uint32_t c0, c1;
   chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
-  if (c0 < c1) emit_chunk(kp, sh, c0, c1);
+  if (c0 >= c1) return;
+  if (LIGHT) emit_light_chunk<DIAG>(kp, sh, c0, c1);
+  else emit_chunk<DIAG>(kp, sh, c0, c1);
 }
+template <bool DIAG, bool LIGHT>
 __global__ __launch_bounds__(kWave) void k_parse_fused(ParseParams kp) {
   __shared__ __attribute__((aligned(16))) ParseShared sh;
   uint32_t c0, c1;
   chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
   if (c0 >= c1) return;
-  scan_chunk(kp, sh, c0, c1);
-  emit_chunk(kp, sh, c0, c1);
+  scan_chunk<DIAG, LIGHT>(kp, sh, c0, c1);
+  if (LIGHT) emit_light_chunk<DIAG>(kp, sh, c0, c1);
+  else emit_chunk<DIAG>(kp, sh, c0, c1);
 }
 
 static int per_cu(const void *k) {
@@ -1074,22 +1264,30 @@ static int per_cu(const void *k) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWave, 0) != hipSuccess) return 1;
   return n > 0 ? n : 1;
 }
-int scan_blocks_per_cu() { return per_cu((const void *)k_scan_tiles); }
-int emit_blocks_per_cu() { return per_cu((const void *)k_emit_tiles); }
-int fused_blocks_per_cu() { return per_cu((const void *)k_parse_fused); }
+// resident one-wave workgroups per CU of the production variants (light = the bench / FFI mode)
+int scan_blocks_per_cu() { return per_cu((const void *)k_scan_tiles<false, true>); }
+int emit_blocks_per_cu() { return per_cu((const void *)k_emit_tiles<false, true>); }
+int fused_blocks_per_cu() { return per_cu((const void *)k_parse_fused<false, true>); }
 
-hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
+template <bool DIAG, bool LIGHT>
+static hipError_t launch(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
   const uint32_t g1 = grid_scan < p.ntiles ? grid_scan : p.ntiles;
   if (grid_emit == 0) {  // fused
-    hipLaunchKernelGGL(k_parse_fused, dim3(g1), dim3(kWave), 0, s, p);
+    hipLaunchKernelGGL((k_parse_fused<DIAG, LIGHT>), dim3(g1), dim3(kWave), 0, s, p);
     return hipGetLastError();
   }
   const uint32_t g2 = grid_emit < p.ntiles ? grid_emit : p.ntiles;
-  hipLaunchKernelGGL(k_scan_tiles, dim3(g1), dim3(kWave), 0, s, p);
+  hipLaunchKernelGGL((k_scan_tiles<DIAG, LIGHT>), dim3(g1), dim3(kWave), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_emit_tiles, dim3(g2), dim3(kWave), 0, s, p);
+  hipLaunchKernelGGL((k_emit_tiles<DIAG, LIGHT>), dim3(g2), dim3(kWave), 0, s, p);
   return hipGetLastError();
+}
+
+hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
+  const bool diag = p.stats || p.stamps, light = (p.flags & kFlagLight) != 0;
+  if (diag) return light ? launch<true, true>(p, grid_scan, grid_emit, s) : launch<true, false>(p, grid_scan, grid_emit, s);
+  return light ? launch<false, true>(p, grid_scan, grid_emit, s) : launch<false, false>(p, grid_scan, grid_emit, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -128,7 +128,7 @@ def load_library(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    p = path or os.environ.get("NPR_LIB") or LIB_PATH  # NPR_LIB: an alternative in-tree build (experiments)
     if not os.path.exists(p):
         raise ImportError(
             f"libnpr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"

@@ -9,7 +9,8 @@ run 900 "gpu_tests_$TAG.log" python -m pytest tests -m gpu -q -x -p no:cacheprov
 rc=$?; [ $rc -eq 0 ] || exit $rc   # any failure may be a device fault: run nothing more
 run 300 "bench_${TAG}.log" python bench.py --steps 50 --warmup 10 --no-cpu || exit $?
 run 300 "bench_${TAG}_stats.log" python bench.py --steps 20 --warmup 5 --no-cpu --stats || exit $?
-cp gpurun_out/stamps_rank0.npy gpurun_out/stamps_${TAG}_fused.npy
-NPR_FUSED=0 run 300 "bench_${TAG}_2k.log" python bench.py --steps 50 --warmup 10 --no-cpu --stats || exit $?
 cp gpurun_out/stamps_rank0.npy gpurun_out/stamps_${TAG}_2k.npy
+NPR_FUSED=1 run 300 "bench_${TAG}_fused.log" python bench.py --steps 50 --warmup 10 --no-cpu --stats || exit $?
+cp gpurun_out/stamps_rank0.npy gpurun_out/stamps_${TAG}_fused.npy
+NPR_LIGHT=1 run 300 "bench_${TAG}_light.log" python bench.py --steps 50 --warmup 10 --no-cpu || exit $?
 exit 0

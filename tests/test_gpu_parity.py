@@ -10,6 +10,8 @@ import json
 import os
 import struct
 
+os.environ.setdefault("NPR_LIGHT", "1")  # exercise the parked-flow mode in the flows_only cases
+
 import numpy as np
 import pytest
 import torch
@@ -31,8 +33,12 @@ def to_dev(blob):
     return t[: len(blob)] if blob else t[:0]
 
 
-def check_parity(blob, start=24, endianness=None, ws=None):
-    """Run the device path on `blob` and compare everything with the oracle."""
+def check_parity(blob, start=24, endianness=None, ws=None, light=False):
+    """Run the device path on `blob` and compare everything with the oracle.
+
+    light=True requests flows only (no record table / status): the launch then runs in the
+    parked-flow mode (pass 1 parks each tile's Ok flows, pass 2 copies them), so the flow table,
+    counts and `consumed` are compared."""
     if start == 24:
         rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
         assert rc == 0
@@ -48,12 +54,19 @@ def check_parity(blob, start=24, endianness=None, ws=None):
     buf = to_dev(blob)
     n = len(blob)
     cap = max((n - start) // 16 + 1, 1)
-    w = ws or device.Workspace(cap, cap, status=True)
+    w = ws or (device.Workspace(cap, cap, records=False, status=False) if light else device.Workspace(cap, cap, status=True))
     w.launch(buf, start=start, endianness=e, nbytes=n)
     sm = w.check()
     assert sm.n_records == len(want_recs), (sm.n_records, len(want_recs))
     assert sm.consumed == want_cons, (sm.consumed, want_cons)
     assert sm.n_flows == len(want_flows)
+    if light:
+        got_flows = w.flows_np()
+        assert got_flows.tobytes() == want_flows.tobytes(), first_diff(got_flows, want_flows)
+        v6mask = (want_flows["kind"] & _abi.KIND_IPV6) != 0
+        if v6mask.any():
+            assert w.flows_v6_np()[v6mask].tobytes() == want_v6[v6mask].tobytes()
+        return sm
     got_recs = w.records_np()
     assert got_recs.tobytes() == want_recs.tobytes(), first_diff(got_recs, want_recs)
     got_status = w.status_np()
@@ -97,72 +110,89 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-def test_c2_small():
-    check_parity(synth.fixed64(50_000))
+LIGHT = pytest.mark.parametrize("light", [False, True], ids=["full", "flows_only"])
 
 
-def test_c3_small():
-    check_parity(synth.variable_mix(20_000))
+@LIGHT
+def test_c2_small(light):
+    check_parity(synth.fixed64(50_000), light=light)
 
 
+@LIGHT
+def test_c3_small(light):
+    check_parity(synth.variable_mix(20_000), light=light)
+
+
+@LIGHT
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_quirk_corpus(seed):
-    check_parity(synth.quirk_corpus(8_000, seed=seed))
+def test_quirk_corpus(seed, light):
+    check_parity(synth.quirk_corpus(8_000, seed=seed), light=light)
 
 
-def test_quirk_corpus_big_endian():
-    check_parity(synth.quirk_corpus(6_000, seed=11, big=True))
+@LIGHT
+def test_quirk_corpus_big_endian(light):
+    check_parity(synth.quirk_corpus(6_000, seed=11, big=True), light=light)
 
 
-def test_adversarial_speculation():
+@LIGHT
+def test_adversarial_speculation(light):
     """Fake record-header chains inside payloads, zero-filled payloads and jumbo (> tile) records
-    defeat the per-tile start speculation; the look-back must still reproduce the serial chain."""
-    check_parity(synth.quirk_corpus(4_000, seed=5, fake_every=3, zero_every=7, jumbo_every=200))
+    defeat the per-tile start speculation; the exact prefix must still reproduce the serial chain."""
+    check_parity(synth.quirk_corpus(4_000, seed=5, fake_every=3, zero_every=7, jumbo_every=200), light=light)
 
 
-def test_jumbo_records_span_many_tiles():
-    check_parity(synth.quirk_corpus(600, seed=6, jumbo_every=2))
+@LIGHT
+def test_jumbo_records_span_many_tiles(light):
+    check_parity(synth.quirk_corpus(600, seed=6, jumbo_every=2), light=light)
 
 
+@LIGHT
 @pytest.mark.parametrize("tail", ["truncated_header", "truncated_payload", "huge_incl"])
-def test_truncated_tails(tail):
-    sm = check_parity(synth.quirk_corpus(3_000, seed=9, tail=tail))
+def test_truncated_tails(tail, light):
+    sm = check_parity(synth.quirk_corpus(3_000, seed=9, tail=tail), light=light)
     assert sm.consumed < len(synth.quirk_corpus(3_000, seed=9, tail=tail))
 
 
-def test_corrupt_incl_mid_file_stops_chain():
+@LIGHT
+def test_corrupt_incl_mid_file_stops_chain(light):
     blob = synth.corrupt_midfile(synth.fixed64(30_000), at_record=12_345)
-    sm = check_parity(blob)
+    sm = check_parity(blob, light=light)
     assert sm.n_records == 12_345
 
 
-def test_empty_and_header_only():
-    check_parity(synth.global_header())                           # 0 records, rem empty
-    check_parity(synth.global_header() + bytes(10))               # 0 records, 10-byte rem
-    check_parity(synth.global_header() + struct.pack("<IIII", 0, 0, 0, 0))  # one zero-length record
+@LIGHT
+def test_empty_and_header_only(light):
+    check_parity(synth.global_header(), light=light)                           # 0 records, rem empty
+    check_parity(synth.global_header() + bytes(10), light=light)               # 0 records, 10-byte rem
+    check_parity(synth.global_header() + struct.pack("<IIII", 0, 0, 0, 0), light=light)  # one zero-length record
 
 
-def test_records_without_file_header():
+@LIGHT
+def test_records_without_file_header(light):
     """PcapRecords::parse(input, endianness) over bare records (start = 0)."""
     body = synth.quirk_corpus(3_000, seed=4, with_header=False)
-    check_parity(body, start=0, endianness=npr.Endianness.Little)
+    check_parity(body, start=0, endianness=npr.Endianness.Little, light=light)
     body = synth.quirk_corpus(3_000, seed=4, with_header=False, big=True)
-    check_parity(body, start=0, endianness=npr.Endianness.Big)
+    check_parity(body, start=0, endianness=npr.Endianness.Big, light=light)
 
 
 def test_workspace_reuse_many_launches():
     blob = synth.quirk_corpus(5_000, seed=21, fake_every=9)
     cap = len(blob) // 16 + 1
     ws = device.Workspace(cap, cap, status=True)
+    wl = device.Workspace(cap, cap, records=False, status=False)
     for _ in range(5):
         check_parity(blob, ws=ws)
+        check_parity(blob, ws=wl, light=True)  # alternate modes on one context
     check_parity(synth.fixed64(10_000), ws=ws)
+    check_parity(synth.fixed64(10_000), ws=wl, light=True)
 
 
-def test_flow_capacity_overflow_reports_exact_counts():
+@pytest.mark.parametrize("records", [True, False], ids=["full", "flows_only"])
+def test_flow_capacity_overflow_reports_exact_counts(records):
     blob = synth.fixed64(5_000)
     buf = to_dev(blob)
-    ws = device.Workspace(10_000, 100)
+    ws = device.Workspace(10_000, 100, records=records)
     ws.launch(buf)
     with pytest.raises(npr.DeviceError):
         ws.check()
