@@ -53,6 +53,20 @@ def cpu_baseline(blob, n_records, budget_s):
                       f"CaptureFile::parse + convert_records, {el:.1f} s on 1 host core"}
 
 
+def pmc_traffic(records):
+    """HBM-side bytes per launch from the newest committed PMC summary of this workload (profiles/),
+    or None.  Collected by scripts/pmc.sh: FETCH_SIZE x2 + WRITE_SIZE summed over both kernels."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if records == 1_000_000 and d.get("workload", "").startswith("C2"):
+            return d.get("traffic_bytes_per_launch"), os.path.basename(f)
+    return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -141,6 +155,7 @@ def main():
         write_b = 32 * n                                    # one 32-B npr_flow per Ok record
         alg = read_b + write_b
         achieved = alg / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(n)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -159,7 +174,8 @@ def main():
                        "outputs": "convert_records flow table (32 B/flow incl. record offset)"},
             "stream_GBps": round(stream_bytes * world * args.steps / wall / 1e9, 2),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "read_only_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": alg, "kernel_ms": round(kern_ms, 5)},
         }

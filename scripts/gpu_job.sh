@@ -17,7 +17,7 @@ run() {  # run <limit-seconds> <log> <cmd...>
 run 900 "gpu_tests_$TAG.log" python -m pytest tests -m gpu -q -x -p no:cacheprovider
 rc=$?
 if [ $rc -ne 0 ]; then echo "tests failed (rc=$rc): stop"; exit $rc; fi
-run 600 "bench_$TAG.json" python bench.py --steps 50 --warmup 10 --stats || exit $?
+run 600 "bench_$TAG.json" python bench.py --steps 50 --warmup 10 || exit $?
 cd /tmp && export TMPDIR=/tmp
 run 600 "rocprof_$TAG.log" rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run \
     --output-format csv -- python3 "$R/bench.py" --steps 50 --warmup 10 --no-cpu || exit $?
