@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NPR_ABI_VERSION 1
+#define NPR_ABI_VERSION 2
 
 /* ---- status of an API call ------------------------------------------------------------ */
 typedef enum npr_status {
@@ -141,7 +141,11 @@ typedef struct npr_summary {
   uint64_t consumed;
   uint32_t flags; /* NPR_SUMMARY_* */
   uint32_t epoch;
+  uint64_t entry; /* offset of the chain's first record (start, or the speculated one of a
+                     speculative-start range; NPR_NO_ENTRY when none was found) */
 } npr_summary;
+
+#define NPR_NO_ENTRY 0xFFFFFFFFFFFFFFFFull
 
 #define NPR_SUMMARY_RECORD_OVERFLOW 0x1u /* record_cap too small */
 #define NPR_SUMMARY_FLOW_OVERFLOW 0x2u   /* flow_cap too small */
@@ -233,6 +237,17 @@ npr_status npr_parse_extract(npr_ctx *ctx, const uint8_t *input, size_t len,
 npr_status npr_dev_parse_extract(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness endianness, const npr_dev_outputs *out,
                                  void *stream);
+/* Byte-range form for sharding one capture: only records that START in
+ * [start, stop) are produced, while payloads may run past `stop` up to `len`.  With
+ * speculative_start != 0, `start` is not known to be a record boundary: the first plausible
+ * record start at or after it is speculated and reported in summary->entry.  The caller checks
+ * it against the previous range's `consumed` and reruns with that exact start when they
+ * differ.  `ref_record` is the offset of a known record header (the capture's first, 24)
+ * whose ts_sec anchors the speculation, or NPR_NO_ENTRY.
+ * npr_dev_parse_extract(start) == this with stop = len, speculative_start = 0, ref = start. */
+npr_status npr_dev_parse_extract_range(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
+                                       uint64_t stop, npr_endianness endianness, int speculative_start,
+                                       uint64_t ref_record, const npr_dev_outputs *out, void *stream);
 /* Synchronise `stream`, copy the summary back and map its flags to a status. */
 npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
                          npr_summary *host_summary);

@@ -256,14 +256,21 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 // ---- device-resident hot path -----------------------------------------------------------------
 npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness e, const npr_dev_outputs *o, void *stream) {
+  return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
+}
+
+npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
+                                       uint64_t stop, npr_endianness e, int speculative_start,
+                                       uint64_t ref_record, const npr_dev_outputs *o, void *stream) {
   if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (stop > len || start > stop) return fail(c, NPR_ERR_ARG, "need start <= stop <= len");
   if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
   if (o->flows && (((uintptr_t)o->flows & 15u) != 0 || (o->flows_v6 && ((uintptr_t)o->flows_v6 & 15u))))
     return fail(c, NPR_ERR_ARG, "flow arrays must be 16-byte aligned");
   if (len >= (1ull << 40)) return fail(c, NPR_ERR_ARG, "input larger than 1 TiB (40-bit record offsets)");
   HIP_CHECK(c, hipSetDevice(c->device));
   uint64_t org = 0;
-  const uint64_t nt = tiles_for(len, start, &org);
+  const uint64_t nt = tiles_for(stop, start, &org);  // tiles cover [org, stop)
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
@@ -295,7 +302,11 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   p.epoch = c->epoch;
   p.ntiles = (uint32_t)nt;
   p.frac_max = 1000000000u;
-  p.flags = start >= 24 ? npr::kFlagMagicAtZero : 0u;  // bytes 0..3 hold the pcap magic
+  p.stop = stop;
+  p.ref = ref_record < len ? ref_record : ~0ull;
+  // a capture file: bytes 0..3 hold the pcap magic (the kernel checks its value)
+  p.flags = (start >= 24 || (ref_record != NPR_NO_ENTRY && ref_record >= 24)) ? npr::kFlagMagicAtZero : 0u;
+  if (speculative_start) p.flags |= npr::kFlagSpecStart;
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
   p.ngroups1 = (uint32_t)ngroups1(nt);

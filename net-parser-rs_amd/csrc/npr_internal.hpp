@@ -41,6 +41,7 @@ struct alignas(32) GroupSlot {
 enum : uint32_t {
   kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
   kFlagLight = 4u,        // flows only (no record table / status): pass 1 parks the flows, pass 2 copies
+  kFlagSpecStart = 8u,    // `start` is not a known record boundary: speculate tile 0's entry too
 };
 
 // optional diagnostic counters (ParseParams::stats, NULL in production launches)
@@ -55,7 +56,9 @@ enum : uint32_t {
 struct ParseParams {
   const uint8_t *buf;  // 16-B aligned device pointer
   uint64_t len;
-  uint64_t start;      // offset of the first record
+  uint64_t start;      // offset of the first record (or where to speculate it, kFlagSpecStart)
+  uint64_t stop;       // only records starting before `stop` belong to this launch (<= len)
+  uint64_t ref;        // a known record header (speculation's ts_sec reference) or ~0
   uint64_t org;        // start rounded down to kTile: tile t covers [org + t*kTile, ...)
   uint32_t big;        // file endianness
   uint32_t epoch;      // granule tag for this launch, 1..65535

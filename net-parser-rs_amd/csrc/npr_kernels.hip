@@ -361,7 +361,7 @@ struct Seg {
 
 __device__ __forceinline__ uint64_t tile_end(const ParseParams &kp, int64_t k) {
   const uint64_t e = kp.org + (uint64_t)(k + 1) * kTile;
-  return e < kp.len ? e : kp.len;
+  return e < kp.stop ? e : kp.stop;
 }
 
 // Chain-consistency monoid: X then Y (Y's tiles follow X's).  Y's counts are trusted only when
@@ -716,8 +716,8 @@ __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
     const uint32_t m = gm.le32(0);
     if (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u) sc.frac_max = 1000000u;
   }
-  sc.has_ref = kp.len >= kp.start + 16;
-  GlobalReader gr{kp.buf + kp.start, sc.has_ref ? 4ull : 0ull};
+  sc.has_ref = kp.ref != kNone && kp.len >= kp.ref + 16;
+  GlobalReader gr{kp.buf + (sc.has_ref ? kp.ref : 0ull), sc.has_ref ? 4ull : 0ull};
   const uint32_t v = gr.le32(0);
   sc.ts_ref = __builtin_amdgcn_readfirstlane(kp.big ? __builtin_bswap32(v) : v);
   sc.frac_max = __builtin_amdgcn_readfirstlane(sc.frac_max);
@@ -728,13 +728,14 @@ __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
 
 // first strong (else first weak) record-start candidate in [0, span) of the staged tile, 64
 // candidates per round; kNone if neither (wave-uniform)
-__device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t span) {
+__device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
+                              uint32_t span) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t avail = kp.len - tile_lo;
   sc.avail = avail > 0xffffffffull ? 0xffffffffu : (uint32_t)avail;
   sc.exact_end = avail <= 0xffffffffull;
   uint32_t weak = 0xffffffffu;
-  for (uint32_t base = 0; base < span; base += 64) {
+  for (uint32_t base = lo; base < span; base += 64) {
     const uint32_t r = base + lane;
     const int g = r < span ? grade(sc, w, r) : 0;
     const uint64_t b2 = __ballot(g == 2);
@@ -823,17 +824,19 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
   uint32_t arrived = 0xffffffffu, arrived_g = 0;   // lane 0: pending group-counter arrival
   auto step = [&](uint32_t t, u32x4 (&q)[kChunks]) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
+    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     stamp<DIAG>(kp, t, 0);
     stage_commit(sh.data, q);
     wave_sync();
     if (t + 2 < c1) stage_issue(kp, tile_lo + 2ull * kTile, q);
 
     uint64_t entry = carry;
-    if (t == 0) {
+    const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
+    if (t == 0 && !spec0) {
       entry = kp.start;
     } else if (carry == kNone) {
-      entry = speculate(sc, kp, sh.data, tile_lo, (uint32_t)(tile_hi - tile_lo));
+      const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
+      entry = tile_hi > tile_lo + lo ? speculate(sc, kp, sh.data, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
       if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
     }
     stamp<DIAG>(kp, t, 1);
@@ -933,11 +936,29 @@ __device__ __forceinline__ void ahead_issue(const ParseParams &kp, uint32_t t, T
   A.a2 = ld_agent(&kp.slots[t].a[2]);
 }
 
+// The chain's anchor: `start`, or with kFlagSpecStart the entry pass 1 speculated for tile 0
+// (none found: the range yields nothing and reports NPR_NO_ENTRY; the chain passes `stop`).
+__device__ bool anchor_of(const ParseParams &kp, Seg &X, uint64_t &entry0, uint64_t t0) {
+  X = start_seg(kp);
+  entry0 = kp.start;
+  if (!(kp.flags & kFlagSpecStart)) return true;
+  for (;;) {
+    const uint64_t a1 = uni64(ld_agent(&kp.slots[0].a[1]));
+    if (tagged(a1, kp.epoch)) {
+      const uint64_t e1 = a1 & kMask48;
+      entry0 = e1 ? e1 - 1 : kNone;
+      X.entry = X.exit = e1 ? e1 - 1 : kp.stop;
+      return true;
+    }
+    if (!spin_ok(kp, t0)) return false;
+  }
+}
+
 // exact chain state before tile c: false when a hand-off timed out
-__device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X) {
+__device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X, uint64_t &entry0) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  X = start_seg(kp);
+  if (!anchor_of(kp, X, entry0, t0)) return false;
   const int64_t h = c >> 12, g = c >> 6;
   if (h > 64) return prefix_generic(kp, X, 0, c, X, t0);  // > 1 GiB before c: the generic walker
   const int n2 = (int)h, n1 = (int)(g - (h << 6)), n0 = (int)((int64_t)c - (g << 6));
@@ -977,11 +998,12 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
   ahead_issue(kp, c0, A);
   if (c0 + 1 < c1) ahead_issue(kp, c0 + 1, B);
   Seg X;
-  if (!prefix_of(kp, c0, X)) return;
+  uint64_t entry0;
+  if (!prefix_of(kp, c0, X, entry0)) return;
   uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
   auto step = [&](uint32_t t, TileAhead &A) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
+    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     stamp<DIAG>(kp, t, 5);
     stage_commit(sh.data, A.q);
     const uint64_t a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: wave-uniform
@@ -1071,6 +1093,7 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
         kp.summary->n_flows = pok;
         kp.summary->consumed = pos;
         kp.summary->flags = fl;
+        kp.summary->entry = entry0;
         kp.summary->epoch = kp.epoch;
       }
     }
@@ -1121,11 +1144,12 @@ __device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseSha
   park_issue(kp, c0, A);
   if (c0 + 1 < c1) park_issue(kp, c0 + 1, B);
   Seg X;
-  if (!prefix_of(kp, c0, X)) return;
+  uint64_t entry0;
+  if (!prefix_of(kp, c0, X, entry0)) return;
   uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
   auto step = [&](uint32_t t, ParkAhead &A) {
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.len ? tile_lo + kTile : kp.len;
+    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     stamp<DIAG>(kp, t, 5);
     const uint64_t a0 = rl64(A.a0, 0), a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: uniform
     const uint32_t ep = kp.epoch;
@@ -1218,6 +1242,7 @@ __device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseSha
         kp.summary->n_flows = pok;
         kp.summary->consumed = pos;
         kp.summary->flags = fl;
+        kp.summary->entry = entry0;
         kp.summary->epoch = kp.epoch;
       }
     }

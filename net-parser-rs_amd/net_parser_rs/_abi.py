@@ -23,9 +23,10 @@ FLOW_DTYPE = np.dtype(
      ("record_offset", "u1", (5,))], align=True)
 FLOW_V6_DTYPE = np.dtype([("src_ip", "u1", (16,)), ("dst_ip", "u1", (16,))])
 SUMMARY_DTYPE = np.dtype([("n_records", "<u8"), ("n_flows", "<u8"), ("consumed", "<u8"),
-                          ("flags", "<u4"), ("epoch", "<u4")])
+                          ("flags", "<u4"), ("epoch", "<u4"), ("entry", "<u8")])
 assert RECORD_DTYPE.itemsize == 24 and FLOW_DTYPE.itemsize == 32 and FLOW_V6_DTYPE.itemsize == 32
-assert SUMMARY_DTYPE.itemsize == 32
+assert SUMMARY_DTYPE.itemsize == 40
+NO_ENTRY = 0xFFFFFFFFFFFFFFFF
 
 KIND_IPV6 = 0x1
 KIND_UDP = 0x2
@@ -73,7 +74,7 @@ class DevOutputsC(ctypes.Structure):
 class SummaryC(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("n_flows", ctypes.c_uint64),
                 ("consumed", ctypes.c_uint64), ("flags", ctypes.c_uint32),
-                ("epoch", ctypes.c_uint32)]
+                ("epoch", ctypes.c_uint32), ("entry", ctypes.c_uint64)]
 
 
 assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24
@@ -84,7 +85,7 @@ EXPORTED = [
     "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps",
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
-    "npr_dev_parse_extract", "npr_dev_check", "npr_dev_extract_flows",
+    "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_check", "npr_dev_extract_flows",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -115,6 +116,9 @@ _SIGNATURES = {
                                          _c_size_p]),
     "npr_dev_parse_extract": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                              ctypes.POINTER(DevOutputsC), _vp]),
+    "npr_dev_parse_extract_range": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                   ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                                   ctypes.POINTER(DevOutputsC), _vp]),
     "npr_dev_check": (ctypes.c_int, [_vp, ctypes.POINTER(DevOutputsC), _vp, ctypes.POINTER(SummaryC)]),
     "npr_dev_extract_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                              _vp, _vp, _vp, _vp]),

@@ -28,7 +28,7 @@ class Workspace:
         self.status = mk(self.record_cap) if status else None
         self.flows = mk(self.flow_cap * 32) if flows else None
         self.flows_v6 = mk(self.flow_cap * 32) if flows_v6 else None
-        self.summary = torch.zeros(32, dtype=torch.uint8, device=self.device)
+        self.summary = torch.zeros(64, dtype=torch.uint8, device=self.device)
         p = lambda t: t.data_ptr() if t is not None else None
         self.outs = _abi.DevOutputsC(p(self.offsets), p(self.records), p(self.status), self.record_cap,
                                      p(self.flows), p(self.flows_v6), self.flow_cap, p(self.summary))
@@ -40,6 +40,21 @@ class Workspace:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         st = self.ctx.lib.npr_dev_parse_extract(self.ctx.handle, buf.data_ptr(), n, start, endianness,
                                                 ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        self.ctx.check(st)
+        self._stream = s
+
+    def launch_range(self, buf, start, stop, endianness=_abi.LITTLE, speculative=False, ref_record=24,
+                     nbytes=None, stream=None):
+        """Records that START in [start, stop) of `buf` (payloads may run past stop): one shard of a
+        capture (npr_dev_parse_extract_range).  speculative=True: `start` is a byte position, the
+        first record at/after it is speculated and reported as summary.entry."""
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        n = buf.numel() if nbytes is None else int(nbytes)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        ref = _abi.NO_ENTRY if ref_record is None else int(ref_record)
+        st = self.ctx.lib.npr_dev_parse_extract_range(self.ctx.handle, buf.data_ptr(), n, int(start), int(stop),
+                                                      endianness, 1 if speculative else 0, ref,
+                                                      ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
 

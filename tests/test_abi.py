@@ -53,7 +53,7 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_hea
         subprocess.run(["gcc", "-std=c11", "-I", os.path.join(REPO, "include"), c, "-o", os.path.join(d, "t")],
                        check=True)
         vals = list(map(int, subprocess.run([os.path.join(d, "t")], capture_output=True, text=True).stdout.split()))
-    assert vals == [24, 24, 32, 32, 32, 64, _abi.FLOW_DTYPE.fields["kind"][1],
+    assert vals == [24, 24, 32, 32, 40, 64, _abi.FLOW_DTYPE.fields["kind"][1],
                     _abi.FLOW_DTYPE.fields["record_offset"][1]]
     import ctypes
     assert ctypes.sizeof(_abi.DevOutputsC) == 64
@@ -61,7 +61,7 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_hea
 
 def test_abi_version():
     lib = _abi.load_library()
-    assert lib.npr_abi_version() == 1
+    assert lib.npr_abi_version() == 2
     assert b"gfx950" in lib.npr_version()
 
 

@@ -1,0 +1,152 @@
+"""The multi-rank path (net_parser_rs.parallel) on CPU: byte-range shards of one capture, the
+one-exchange reconcile, the reverse-rank merge.  The oracle stands in for each rank's device
+parse here (test infrastructure only); tests/test_gpu_parallel.py runs the same logic over the
+device range API.  world_size 2 runs over torch.distributed `gloo` at 127.0.0.1."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import _oracle
+from net_parser_rs import _abi, parallel, synth
+
+
+def full_reference(blob):
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    assert rc == 0
+    flows, v6 = _oracle.convert_records(blob, recs)
+    return hdr, recs, cons, flows
+
+
+def oracle_local(blob, endianness, spec):
+    """Rank-local parser over the oracle: records that start in [start, hi) of the chain from
+    `start`; with speculative=True the start comes from `spec(lo, hi)` (right or wrong on purpose)."""
+    def local(lo, hi, start, speculative):
+        if speculative:
+            start = spec(lo, hi)
+            if start is None:
+                return parallel.ShardResult(_abi.NO_ENTRY, hi, 0, 0, np.zeros(0, _abi.FLOW_DTYPE))
+        recs, cons = _oracle.records_parse(blob[start:], endianness)
+        recs = recs.copy()
+        recs["offset"] += start
+        keep = recs[recs["offset"] < hi]
+        consumed = int(recs["offset"][len(keep)]) if len(keep) < len(recs) else start + cons
+        flows, _ = _oracle.convert_records(blob, keep)
+        return parallel.ShardResult(start, consumed, len(keep), len(flows), flows)
+    return local
+
+
+def spec_exact(recs):
+    offs = np.asarray(recs["offset"], dtype=np.int64)
+
+    def spec(lo, hi):  # the true first record start in [lo, hi)
+        i = np.searchsorted(offs, lo)
+        return int(offs[i]) if i < len(offs) and offs[i] < hi else lo
+    return spec
+
+
+def spec_off_by(recs, skip):
+    exact = spec_exact(recs)
+    offs = np.asarray(recs["offset"], dtype=np.int64)
+
+    def spec(lo, hi):  # a WRONG guess: `skip` records late (a plausible but mis-aligned chain)
+        e = exact(lo, hi)
+        i = np.searchsorted(offs, e)
+        return int(offs[min(i + skip, len(offs) - 1)])
+    return spec
+
+
+def check_merge(blob, world, spec_maker):
+    hdr, recs, cons, flows = full_reference(blob)
+    local = oracle_local(blob, hdr.endianness, spec_maker(recs))
+    results, live, rounds = parallel.parse_sharded_inprocess(local, 24, len(blob), world)
+    merged = parallel.merge_flows(results, live)
+    _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
+    assert r_tot == len(recs) and f_tot == len(flows)
+    assert merged.tobytes() == flows.tobytes()
+    return rounds
+
+
+@pytest.mark.parametrize("world", [2, 3, 5, 8])
+def test_sharded_matches_serial_with_right_speculation(world):
+    rounds = check_merge(synth.quirk_corpus(3_000, seed=31), world, spec_exact)
+    assert rounds == 1  # one exchange, no rerun
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_wrong_speculation_is_rerun(world):
+    rounds = check_merge(synth.quirk_corpus(3_000, seed=32), world, lambda recs: spec_off_by(recs, 1))
+    assert rounds > 1
+
+
+def test_no_speculated_start():
+    check_merge(synth.quirk_corpus(2_000, seed=33), 3, lambda recs: (lambda lo, hi: None))
+
+
+def test_chain_end_inside_a_shard_stops_later_ranks():
+    blob = synth.corrupt_midfile(synth.fixed64(4_000), at_record=700)   # END early: rank 0's range
+    check_merge(blob, 4, spec_exact)
+
+
+def test_jumbo_records_cross_shards():
+    check_merge(synth.quirk_corpus(300, seed=34, jumbo_every=2), 6, spec_exact)
+
+
+def test_replay_pure():
+    bounds = [(24, 100), (100, 200), (200, 300)]
+    ok = [parallel.ShardResult(24, 110, 3, 3), parallel.ShardResult(110, 205, 2, 1),
+          parallel.ShardResult(205, 300, 2, 2)]
+    assert parallel.replay(24, bounds, ok)[0] is None
+    bad = list(ok)
+    bad[2] = parallel.ShardResult(204, 300, 2, 2)
+    r, e, _ = parallel.replay(24, bounds, bad)
+    assert (r, e) == (2, 205)
+    ended = [parallel.ShardResult(24, 90, 3, 3), parallel.ShardResult(110, 205, 2, 1),
+             parallel.ShardResult(205, 300, 2, 2)]
+    r, e, live = parallel.replay(24, bounds, ended)
+    assert r is None and live == [True, False, False]
+
+
+# ---- world_size 2 over gloo (one process per rank, 127.0.0.1) ----------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, blob, wrong, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hdr, recs, cons, flows = full_reference(blob)
+        spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
+        local = oracle_local(blob, hdr.endianness, spec)
+        mine, metas, live, rounds = parallel.parse_sharded(local, 24, len(blob))
+        merged = parallel.gather_flows(mine, metas, live)
+        if rank == 0:
+            _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
+            q.put((r_tot == len(recs), f_tot == len(flows), merged.tobytes() == flows.tobytes(), rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wrong", [False, True], ids=["exact", "rerun"])
+def test_gloo_world2(wrong):
+    blob = synth.quirk_corpus(2_500, seed=35)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, blob, wrong, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    recs_ok, flows_ok, bytes_ok, rounds = q.get(timeout=10)
+    assert recs_ok and flows_ok and bytes_ok
+    assert (rounds > 1) == wrong
