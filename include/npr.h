@@ -184,9 +184,10 @@ const char *npr_ctx_last_error(const npr_ctx *ctx);
 npr_status npr_ctx_set_stats(npr_ctx *ctx, int enable);
 npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
 /* With npr_ctx_set_stats(ctx, 2): per-tile s_memrealtime (100 MHz) stamps of the last parse,
- * 8 words per tile: pass 1 [0] tile start [1] entry known [2] walked [3] counted [4] published;
- * pass 2 [5] tile start [6] record offsets known [7] written.  out may be NULL with cap 0 to
- * query *n_tiles only. */
+ * 16 words per tile: pass 1 [0] tile start [1] entry known [2] walked [3] counted [4] published;
+ * pass 2 [5] tile start [6] record offsets known [7] written; on the first tile of a wave's
+ * chunk: [8] pass-2 entry [9] prologue issued [10] prefix known [11]/[12] pass-1 group arrival
+ * start/end.  out may be NULL with cap 0 to query *n_tiles only. */
 npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_tiles);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

@@ -201,7 +201,7 @@ npr_status npr_ctx_read_stamps(npr_ctx *c, uint64_t *out, uint64_t cap, uint64_t
   if (!c->stamps.p) return fail(c, NPR_ERR_ARG, "stamps not enabled (npr_ctx_set_stats(ctx, 2))");
   HIP_CHECK(c, hipSetDevice(c->device));
   HIP_CHECK(c, hipDeviceSynchronize());
-  const uint64_t n = std::min<uint64_t>(cap, c->stamp_tiles * 8);
+  const uint64_t n = std::min<uint64_t>(cap, c->stamp_tiles * npr::kStampWords);
   if (n) HIP_CHECK(c, hipMemcpy(out, c->stamps.p, n * 8, hipMemcpyDeviceToHost));
   if (n_tiles) *n_tiles = c->stamp_tiles;
   return NPR_OK;
@@ -331,7 +331,7 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   p.stats = c->stats;
   p.stamps = nullptr;
   if (c->stats_mode >= 2) {
-    if ((st = ensure(c, c->stamps, nt * 64, true))) return st;
+    if ((st = ensure(c, c->stamps, nt * npr::kStampWords * 8, true))) return st;
     p.stamps = (uint64_t *)c->stamps.p;
     c->stamp_tiles = nt;
   }

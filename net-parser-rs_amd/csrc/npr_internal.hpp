@@ -52,6 +52,7 @@ enum : uint32_t {
   kStatNoEntry = 5,    // tiles with no plausible record start
   kStatCount = 8
 };
+constexpr int kStampWords = 16;  // diagnostic stamps per tile (npr_ctx_read_stamps)
 
 struct ParseParams {
   const uint8_t *buf;  // 16-B aligned device pointer

@@ -272,35 +272,40 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
     a[k] = __builtin_amdgcn_alignbyte(nx, prev, sh);
     prev = nx;
   }
+  // pin the window in registers: otherwise the backend turns the IPv4/IPv6 selects below into
+  // divergent branches that each load only their own words (select-to-branch on loads)
+#pragma unroll
+  for (int k = 0; k < 17; ++k) asm volatile("" : "+v"(a[k]));
   auto byte = [&](int i) { return (a[i >> 2] >> (8 * (i & 3))) & 0xffu; };
   auto be16 = [&](int i) { return (byte(i) << 8) | byte(i + 1); };
+  // Every quantity is computed for every lane and combined by selects (no data-dependent
+  // branches: divergent if/else here costs more scalar exec-mask work than the arithmetic).
   const uint32_t etype = be16(12), b0 = byte(14);
   const uint32_t proto4 = byte(23), nh = byte(20);
-  const bool v4 = etype == 0x0800u && b0 == 0x45u && n >= 34u && (proto4 == 6u || proto4 == 17u);
-  const bool v6 = etype == 0x86ddu && (b0 >> 4) == 6u && n >= 54u && (nh == 6u || nh == 17u);
-  if (!(v4 || v6)) return 0xffu;
+  const bool v4 = (etype == 0x0800u) & (b0 == 0x45u) & (n >= 34u) & ((proto4 == 6u) | (proto4 == 17u));
+  const bool v6 = (etype == 0x86ddu) & ((b0 >> 4) == 6u) & (n >= 54u) & ((nh == 6u) | (nh == 17u));
   const uint32_t n3 = n - 14u;
   // IPv4 (IHL 5): wrapping u16 payload length; options/padding absent -> never a remainder
   const uint32_t length = v4 ? ((be16(16) - 20u) & 0xffffu) : be16(18);
   const uint32_t hl3 = v4 ? 20u : 40u;
-  const uint32_t st3 = (n3 - hl3 < length) ? (v4 ? NPR_FLOW_L2_IPV4_INCOMPLETE : NPR_FLOW_L2_IPV6_INCOMPLETE)
-                       : (!v4 && n3 - hl3 != length) ? (uint32_t)NPR_FLOW_L2_IPV6_REMAINDER : 0u;
+  const bool l3_short = n3 - hl3 < length, l3_rem = !v4 & (n3 - hl3 != length);
+  const uint32_t st3 = l3_short ? (v4 ? (uint32_t)NPR_FLOW_L2_IPV4_INCOMPLETE : (uint32_t)NPR_FLOW_L2_IPV6_INCOMPLETE)
+                                : (l3_rem ? (uint32_t)NPR_FLOW_L2_IPV6_REMAINDER : 0u);
   const uint32_t proto = v4 ? proto4 : nh;
   const uint32_t n4 = length;
   const uint32_t hv = v4 ? be16(46) : be16(66);
   const uint32_t ulen = v4 ? be16(38) : be16(58);
   const uint32_t thl = (hv >> 12) * 4u;
   const uint32_t off = v4 ? 0u : 3u;  // the IPv6 TCP/UDP leaves are 3 codes after the IPv4 ones
-  uint32_t st4;
-  if (proto == 6u)
-    st4 = n4 < 14u ? NPR_FLOW_L3_IPV4_TCP_INCOMPLETE + off
-          : (thl < 20u || thl > 60u) ? NPR_FLOW_L3_IPV4_TCP_FAILURE + off
-          : n4 < thl ? NPR_FLOW_L3_IPV4_TCP_INCOMPLETE + off : 0u;
-  else
-    st4 = n4 < 8u ? NPR_FLOW_L3_IPV4_UDP_INCOMPLETE + off
-          : (ulen < 8u || n4 - 8u < ulen - 8u) ? NPR_FLOW_L3_IPV4_UDP_INCOMPLETE + off
-          : n4 != ulen ? (v4 ? (uint32_t)NPR_FLOW_L3_IPV4_UDP_REMAINDER : (uint32_t)NPR_FLOW_L3_IPV6_UDP_REMAINDER)
-                       : 0u;
+  // TCP (src/layer4/tcp.rs:59-101): 14 bytes, data offset in [20, 60], then the whole header
+  const bool t_short = n4 < 14u, t_bad = (thl < 20u) | (thl > 60u);
+  const uint32_t st_tcp = t_short ? NPR_FLOW_L3_IPV4_TCP_INCOMPLETE + off
+                        : (t_bad ? NPR_FLOW_L3_IPV4_TCP_FAILURE + off : (n4 < thl ? NPR_FLOW_L3_IPV4_TCP_INCOMPLETE + off : 0u));
+  // UDP (src/layer4/udp.rs:33-50): OK iff 8 <= L == payload length
+  const bool u_inc = (n4 < 8u) | (ulen < 8u) | (n4 - 8u < ulen - 8u);
+  const uint32_t st_udp = u_inc ? NPR_FLOW_L3_IPV4_UDP_INCOMPLETE + off
+                        : (n4 != ulen ? (v4 ? (uint32_t)NPR_FLOW_L3_IPV4_UDP_REMAINDER : (uint32_t)NPR_FLOW_L3_IPV6_UDP_REMAINDER) : 0u);
+  const uint32_t st4 = proto == 6u ? st_tcp : st_udp;
   if (FIELDS) {
     const uint32_t sp = v4 ? be16(34) : be16(54), dp = v4 ? be16(36) : be16(56);
     f.d[0] = v4 ? __builtin_amdgcn_alignbyte(a[7], a[6], 2) : 0u;  // IPv4 src, bytes 26..29
@@ -309,23 +314,25 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
     f.d[3] = a[1] & 0xffff0000u;  // vlan 0 | src mac 0..1
     f.d[4] = a[2];
     f.d[5] = a[0];
-    f.d[6] = (a[1] & 0xffffu) | (((v6 ? NPR_FLOW_KIND_IPV6 : 0u) | (proto == 17u ? NPR_FLOW_KIND_UDP : 0u)) << 16);
+    f.d[6] = (a[1] & 0xffffu) | ((((v6 ? NPR_FLOW_KIND_IPV6 : 0u) | (proto == 17u ? NPR_FLOW_KIND_UDP : 0u))) << 16);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f.v6[k] = __builtin_amdgcn_alignbyte(a[6 + k], a[5 + k], 2);  // bytes 22..53
   }
-  return st3 ? st3 : st4;
+  return (v4 | v6) ? (st3 ? st3 : st4) : 0xffu;
 }
 
 // one record (header at LDS offset rel) -> status (+ flow words); fast shape first
 template <bool FIELDS>
 __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo,
-                                               uint32_t rel, FlowWords &f) {
+                                               uint32_t rel, FlowWords &f, bool valid = true) {
   const uint32_t incl = hdr(w, rel, 2, kp.big);
   uint32_t st = decode_fast<FIELDS>(w, rel + 16u, incl, f);
-  if (st == 0xffu) {
-    const uint64_t p = tile_lo + rel;
-    TileReader r{w, (const uint8_t *)w, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
-    st = decode<FIELDS>(r, incl, f);
+  if (__ballot(valid && st == 0xffu)) {  // uniform test: most tiles never take the general path
+    if (valid && st == 0xffu) {
+      const uint64_t p = tile_lo + rel;
+      TileReader r{w, (const uint8_t *)w, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
+      st = decode<FIELDS>(r, incl, f);
+    }
   }
   return st;
 }
@@ -643,23 +650,27 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
     const uint32_t stride = 16u + incl;
     uint64_t b[kWalkUnroll];
     uint32_t qr[kWalkUnroll];
+    uint32_t h[kWalkUnroll];
 #pragma unroll
-    for (int u = 0; u < kWalkUnroll; ++u) {
-      const uint32_t k = lane + 64u * (uint32_t)u;
-      qr[u] = r + k * stride;  // < 2^24: k < 256, stride <= 16 + kTile
-      bool ok = k == 0;
-      if (k != 0 && qr[u] < span) ok = hdr(w, qr[u], 2, big) == incl && avail - qr[u] >= stride;
-      b[u] = __ballot(ok);
+    for (int u = 0; u < kWalkUnroll; ++u) {  // all header reads issued together, unconditionally
+      qr[u] = r + (lane + 64u * (uint32_t)u) * stride;  // < 2^24: k < 256, stride <= 16 + kTile
+      h[u] = hdr(w, qr[u] < span ? qr[u] : 0u, 2, big);
     }
+#pragma unroll
+    for (int u = 0; u < kWalkUnroll; ++u) asm volatile("" : "+v"(h[u]));  // no load sinking
+#pragma unroll
+    for (int u = 0; u < kWalkUnroll; ++u)  // bitwise, not short-circuit: no branches
+      b[u] = __ballot(((lane == 0) & (u == 0)) | ((qr[u] < span) & (h[u] == incl) & (avail - qr[u] >= stride)));
     uint32_t m = 0;
 #pragma unroll
     for (int u = 0; u < kWalkUnroll; ++u) {
       if (m != 64u * (uint32_t)u) break;
       m += (~b[u] == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~b[u]);
     }
+    // unconditional stores: lanes past m write beyond the chain's records, into slots the next
+    // step (or nothing) overwrites; srec holds 2 * kMaxRec entries so no index overflows
 #pragma unroll
-    for (int u = 0; u < kWalkUnroll; ++u)
-      if (lane + 64u * (uint32_t)u < m) srec[n + lane + 64u * (uint32_t)u] = (uint16_t)qr[u];
+    for (int u = 0; u < kWalkUnroll; ++u) srec[n + lane + 64u * (uint32_t)u] = (uint16_t)qr[u];
     n += m;
     p += (uint64_t)m * stride;
   }
@@ -670,7 +681,7 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
 // diagnostics (DIAG kernel variants only: the production kernels carry none of this)
 template <bool DIAG>
 __device__ __forceinline__ void stamp(const ParseParams &kp, uint32_t t, int k) {
-  if (DIAG && kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * 8 + k] = __builtin_amdgcn_s_memrealtime();
+  if (DIAG && kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * kStampWords + k] = __builtin_amdgcn_s_memrealtime();
 }
 
 // LDS written by some lanes of this wave, then read by others: LDS executes one wave's requests
@@ -695,14 +706,12 @@ __device__ __forceinline__ void stage_issue(const ParseParams &kp, uint64_t tile
   for (int i = 0; i < kChunks; ++i)
     q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((lane + 64u * (uint32_t)i) * 16u), 0, 0);
 }
+// The LDS stage holds kChunks full 1-KiB rows (>= kStage bytes): every chunk is stored
+// unconditionally; chunks past the input / the stage were loaded out of range and are 0.
 __device__ __forceinline__ void stage_commit(uint32_t *data, const u32x4 (&q)[kChunks]) {
   const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
-  for (int i = 0; i < kChunks; ++i) {
-    const uint32_t c = lane + 64u * (uint32_t)i;
-    if (c < kStage / 16) *reinterpret_cast<u32x4 *>(&data[c * 4]) = q[i];
-  }
-  if (lane < 4) data[kStage / 4 + lane] = 0;
+  for (int i = 0; i < kChunks; ++i) *reinterpret_cast<u32x4 *>(&data[(lane + 64u * (uint32_t)i) * 4]) = q[i];
 }
 
 // speculation context of this launch: ts_usec bound from the file magic, the first record's
@@ -758,9 +767,60 @@ __device__ __forceinline__ void put_v6(uint32_t *row, const FlowWords &f) {
   d[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
 }
 
+// ---- LDS-DMA staging ring (per wave) -------------------------------------------------------
+// Tiles land in LDS straight from HBM (`buffer_load_dwordx4 ... lds`, 1 KiB per instruction,
+// range-checked: bytes past the input read 0) with no registers held in flight.  The next
+// tile's DMA is issued before the wait for the current one, so the youngest vector-memory
+// instructions at the wait are exactly the next tiles' DMAs: `s_waitcnt vmcnt(k * per-tile)`
+// retires the current tile and nothing later, whatever stores came before.
+#ifndef NPR_RING
+#define NPR_RING 2
+#endif
+constexpr int kRing = NPR_RING;       // tiles staged per wave (1 processed + kRing-1 in flight)
+constexpr int kRows = kTile / 1024;   // 1-KiB rows of a tile (16-B DMA), then one 256-B halo row (4-B DMA)
+constexpr int kSlotWords = kTile / 4 + 64;
+constexpr int kDmaScan = kRows + 1;   // DMA instructions per tile, pass 1
+constexpr int kDmaEmit = kRows + 4;   // + 2 record-offset rows + 1 aggregate row, pass 2
+static_assert(kTile % 1024 == 0 && kHalo <= 256 - 80, "halo row must hold the halo + the decode over-read");
+typedef __attribute__((address_space(3))) void *lds_ptr_t;
+
+__device__ __forceinline__ void dma_tile(const ParseParams &kp, uint64_t tile_lo, uint32_t *dst) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t avail = kp.len > tile_lo ? kp.len - tile_lo : 0;
+  const uint32_t nbytes = avail < (uint64_t)kStage ? (uint32_t)avail : (uint32_t)kStage;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + tile_lo), 0, (int)((nbytes + 15u) & ~15u), 0x00020000);
+#pragma unroll
+  for (int i = 0; i < kRows; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + i * 256), 16, (lane + 64u * (uint32_t)i) * 16u, 0, 0, 0);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + kRows * 256), 4, (uint32_t)kTile + lane * 4u, 0, 0, 0);
+}
+// pass 2 extras: pass 1's record-offset pairs of tile t and its A granules (dwords 0..5), sc1
+__device__ __forceinline__ void dma_extras(const ParseParams &kp, uint32_t t, uint32_t *off, uint32_t *agg) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, kMaxRec * 2, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)off, 4, lane * 4u, 0, 0, 16);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)(off + 64), 4, lane * 4u + 256u, 0, 0, 16);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.slots + t), 0, 24, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)agg, 4, lane * 4u, 0, 0, 16);
+}
+// wait until at most `ahead` tiles' DMAs (of `per` instructions each) are outstanding
+template <int PER>
+__device__ __forceinline__ void wait_dma(uint32_t ahead) {
+  constexpr int w1 = PER, w2 = 2 * PER;
+  static_assert(2 * PER < 64, "vmcnt field is 6 bits");
+  if (ahead == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
+  else if (ahead == 1 || kRing <= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (w1 & 15) | ((w1 >> 4) << 14));
+  else __builtin_amdgcn_s_waitcnt(0x0F70 | (w2 & 15) | ((w2 >> 4) << 14));
+  wave_sync();  // LDS reads of the landed tile stay below the wait
+}
+
 struct ParseShared {  // one wave's LDS
-  uint32_t data[kStage / 4 + 4];
-  uint16_t srec[kMaxRec];
+  uint32_t data[kRing][kSlotWords];     // tile + 256-B halo row (>= kStage bytes + the decoder's 72-B over-read)
+  uint32_t off[kRing][kMaxRec / 2];     // pass 2: pass 1's record-offset pairs (DMA)
+  uint32_t agg[kRing][64];              // pass 2: the tile's A granules (DMA, dwords 0..5)
+  uint16_t srec[2 * kMaxRec];           // record offsets (+ room for the walk's unconditional stores)
 };
 
 __device__ __forceinline__ void publish_fold(const ParseParams &kp, GroupSlot *G, const Seg &c, int64_t first) {
@@ -804,31 +864,31 @@ __device__ __forceinline__ void fold_groups(const ParseParams &kp, uint32_t g) {
 
 // ---------------------------------------------------------------------------------------------
 // pass 1: scan_chunk — ONE WAVE owns the contiguous tiles [c0, c1) and never waits on another
-// wave (no workgroup barriers anywhere).  Per tile: (tile + 2 -> registers) | entry = the
+// wave (no workgroup barriers anywhere).  Per tile: (the next tile -> LDS by DMA) | entry = the
 // previous tile's exit while the chain continues, else a speculated start | walk -> record
-// offsets, also kept in the offset scratch for pass 2 | status-only decode -> Ok count |
-// publish A = {entry, exit, n, Ok count} and arrive at the group counter.  The arrival's
-// returned value is consumed one tile later (its round trip overlaps the next tile): the last
-// arriver of a 64-tile group folds G1, the last group of a 4096-tile block folds G2.
+// offsets, also kept in the offset scratch for pass 2 | status-only decode -> Ok count (light
+// mode: decode with fields, Ok flows parked) | publish A = {entry, exit, n, Ok count}.  At the
+// end of the chunk the wave arrives once at each 64-tile group it touched: the arrival that
+// completes a group folds its G1, and the group that completes a 4096-tile block folds G2.
 // ---------------------------------------------------------------------------------------------
 template <bool DIAG, bool LIGHT>
 __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
   const uint32_t lane = threadIdx.x & 63u;
-  // two tiles in flight: register sets qa / qb alternate (the loop is unrolled by two so the
-  // compiler counts the loads it waits for)
-  u32x4 qa[kChunks], qb[kChunks];
-  stage_issue(kp, kp.org + (uint64_t)c0 * kTile, qa);
-  if (c0 + 1 < c1) stage_issue(kp, kp.org + (uint64_t)(c0 + 1) * kTile, qb);
+#pragma unroll
+  for (int k = 0; k < kRing - 1; ++k)
+    if (c0 + k < c1) dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
   const SpecCtx sc = spec_ctx(kp);
-  uint64_t carry = kNone;                          // exact continuation of the chain
-  uint32_t arrived = 0xffffffffu, arrived_g = 0;   // lane 0: pending group-counter arrival
-  auto step = [&](uint32_t t, u32x4 (&q)[kChunks]) {
+  uint64_t carry = kNone;  // exact continuation of the chain
+  for (uint32_t t = c0; t < c1; ++t) {
+    const uint32_t slot = (t - c0) % kRing;
+    const uint32_t *w = sh.data[slot];
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     stamp<DIAG>(kp, t, 0);
-    stage_commit(sh.data, q);
-    wave_sync();
-    if (t + 2 < c1) stage_issue(kp, tile_lo + 2ull * kTile, q);
+    // refill the slot processed last iteration with the tile kRing-1 ahead, then wait for this one
+    const uint32_t ahead = c1 - 1 - t < (uint32_t)(kRing - 1) ? c1 - 1 - t : (uint32_t)(kRing - 1);
+    if (t + kRing - 1 < c1) dma_tile(kp, tile_lo + (uint64_t)(kRing - 1) * kTile, sh.data[(slot + kRing - 1) % kRing]);
+    wait_dma<kDmaScan>(ahead);
 
     uint64_t entry = carry;
     const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
@@ -836,38 +896,35 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       entry = kp.start;
     } else if (carry == kNone) {
       const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
-      entry = tile_hi > tile_lo + lo ? speculate(sc, kp, sh.data, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+      entry = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
       if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
     }
     stamp<DIAG>(kp, t, 1);
     entry = uni64(entry);
     uint32_t n = 0;
     uint64_t ex = entry == kNone ? 0ull : entry;
-    if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, entry, n);
+    if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, entry, n);
     ex = uni64(ex);
     wave_sync();
     stamp<DIAG>(kp, t, 2);
 
     // ---- full mode: offsets -> scratch (pairs of u16) + Ok count (status-only decode);
     //      light mode: decode with fields, Ok flows parked in tile order
-    if (!LIGHT && kp.srec_g) {
-      uint32_t *dst = reinterpret_cast<uint32_t *>(kp.srec_g + (uint64_t)t * kMaxRec);
+    if (!LIGHT && kp.srec_g) {  // (n + 1) / 2 offset pairs; the descriptor's range drops the rest
       const uint32_t *src = reinterpret_cast<const uint32_t *>(sh.srec);
-      const uint32_t np = (n + 1) / 2;  // <= kMaxRec / 2 = 2 * 64 pairs
-      if (lane < np) dst[lane] = src[lane];
-      if (lane + 64 < np) dst[lane + 64] = src[lane + 64];
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          (void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, (int)(((n + 1) / 2) * 4u), 0x00020000);
+      __builtin_amdgcn_raw_buffer_store_b32(src[lane], rs, (int)(lane * 4u), 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b32(src[lane + 64], rs, (int)(lane * 4u + 256u), 0, 0);
     }
     uint32_t okc = 0;
     for (int s = 0; s < kRounds; ++s) {
       if ((uint32_t)s * 64u >= n) break;
       const uint32_t i = lane + (uint32_t)s * 64u;
-      bool ok = false;
+      const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
       FlowWords f;
-      uint32_t rel = 0;
-      if (i < n) {
-        rel = sh.srec[i];
-        ok = decode_rec<LIGHT>(kp, sh.data, tile_lo, rel, f) == NPR_FLOW_OK;
-      }
+      const uint32_t rel = sh.srec[i];
+      const bool ok = decode_rec<LIGHT>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
       const uint64_t bal = __ballot(ok);
       if (LIGHT && ok) {
         const uint32_t r = okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
@@ -880,33 +937,29 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       okc += (uint32_t)__builtin_popcountll(bal);
     }
     stamp<DIAG>(kp, t, 3);
-    uint32_t fold = 0xffffffffu;
     if (lane == 0) {
-      TileSlot *slot = kp.slots + t;
+      TileSlot *slot_t = kp.slots + t;
       const uint32_t ep = kp.epoch;
-      st_agent(&slot->a[0], gran(ep, ex));
-      st_agent(&slot->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
-      st_agent(&slot->a[2], gran(ep, (uint64_t)n | ((uint64_t)okc << 24)));
-      // the previous tile's arrival has returned by now: was it its group's last?
-      if (arrived != 0xffffffffu && arrived == group_size(kp, arrived_g) - 1u) fold = arrived_g;
-      arrived_g = t >> 6;
-      arrived = __hip_atomic_fetch_add(kp.cnt1 + 2 * arrived_g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_agent(&slot_t->a[0], gran(ep, ex));
+      st_agent(&slot_t->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
+      st_agent(&slot_t->a[2], gran(ep, (uint64_t)n | ((uint64_t)okc << 24)));
     }
     // the chain continues into the next tile unless it ended here (Q3) or nothing was found
     carry = uni64((entry != kNone && ex >= tile_hi) ? ex : kNone);
-    fold = __builtin_amdgcn_readfirstlane(fold);
-    if (fold != 0xffffffffu) fold_groups(kp, fold);
     stamp<DIAG>(kp, t, 4);
-    wave_sync();  // done with this tile's LDS before the next commit
-  };
-  for (uint32_t t = c0; t < c1; t += 2) {
-    step(t, qa);
-    if (t + 1 < c1) step(t + 1, qb);
+    wave_sync();  // done with this slot's LDS before it is refilled
   }
-  uint32_t fold = 0xffffffffu;
-  if (lane == 0 && arrived == group_size(kp, arrived_g) - 1u) fold = arrived_g;
-  fold = __builtin_amdgcn_readfirstlane(fold);
-  if (fold != 0xffffffffu) fold_groups(kp, fold);
+  // arrive at the chunk's groups (one add per group; the add that completes a group folds it)
+  stamp<DIAG>(kp, c0, 11);
+  for (uint32_t g = c0 >> 6; g <= (c1 - 1) >> 6; ++g) {
+    const uint32_t lo = c0 > (g << 6) ? c0 : (g << 6), hi = c1 < ((g + 1) << 6) ? c1 : ((g + 1) << 6);
+    uint32_t last = 0;
+    if (lane == 0)
+      last = __hip_atomic_fetch_add(kp.cnt1 + 2 * g, hi - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (hi - lo) ==
+             group_size(kp, g);
+    if (__builtin_amdgcn_readfirstlane(last)) fold_groups(kp, g);
+  }
+  stamp<DIAG>(kp, c0, 12);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -914,28 +967,11 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
 //   exact prefix before c0 = start ⊕ G2(blocks) ⊕ G1(groups) ⊕ A(tiles): the three 64-wide
 //   windows are loaded together, then folded; a contradiction (a mis-speculated tile m < c0)
 //   is settled by m's exact prefix P(m), published below by m's owner.  Then per tile,
-//   carrying the exact chain position and counts: (tile + 2, its A and its record offsets ->
-//   registers) | the offsets: pass 1's when its entry equals the exact position (the common
-//   case), else a walk | decode every record | record table / status | Ok flows at their
-//   convert_records (reverse-order) positions, ranked by ballot | publish P(t).
+//   carrying the exact chain position and counts: (the next tile, its A granules and pass 1's
+//   record offsets -> LDS by DMA) | the offsets: pass 1's when its entry equals the exact
+//   position (the common case), else a walk | decode every record | record table / status |
+//   Ok flows at their convert_records (reverse-order) positions, ranked by ballot | publish P(t).
 // ---------------------------------------------------------------------------------------------
-struct TileAhead {  // what pass 2 prefetches for a tile
-  u32x4 q[kChunks];
-  uint32_t off0, off1;  // record-offset pairs lane, lane + 64 from the scratch
-  uint64_t a1, a2;      // A granules: entry + 1, n | okc << 24
-};
-
-__device__ __forceinline__ void ahead_issue(const ParseParams &kp, uint32_t t, TileAhead &A) {
-  const uint32_t lane = threadIdx.x & 63u;
-  stage_issue(kp, kp.org + (uint64_t)t * kTile, A.q);
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, kMaxRec * 2, 0x00020000);
-  A.off0 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u), 0, 16);  // sc1: L2-served
-  A.off1 = __builtin_amdgcn_raw_buffer_load_b32(rs, (int)(lane * 4u + 256u), 0, 16);
-  A.a1 = ld_agent(&kp.slots[t].a[1]);
-  A.a2 = ld_agent(&kp.slots[t].a[2]);
-}
-
 // The chain's anchor: `start`, or with kFlagSpecStart the entry pass 1 speculated for tile 0
 // (none found: the range yields nothing and reports NPR_NO_ENTRY; the chain passes `stop`).
 __device__ bool anchor_of(const ParseParams &kp, Seg &X, uint64_t &entry0, uint64_t t0) {
@@ -994,38 +1030,49 @@ __device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X, uint64_t &e
 template <bool DIAG>
 __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
   const uint32_t lane = threadIdx.x & 63u;
-  TileAhead A, B;  // two tiles in flight (the loop is unrolled by two)
-  ahead_issue(kp, c0, A);
-  if (c0 + 1 < c1) ahead_issue(kp, c0 + 1, B);
+  stamp<DIAG>(kp, c0, 8);
+#pragma unroll
+  for (int k = 0; k < kRing - 1; ++k)
+    if (c0 + k < c1) {
+      dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
+      dma_extras(kp, c0 + k, sh.off[k], sh.agg[k]);
+    }
   Seg X;
   uint64_t entry0;
+  stamp<DIAG>(kp, c0, 9);
   if (!prefix_of(kp, c0, X, entry0)) return;
+  stamp<DIAG>(kp, c0, 10);
   uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
-  auto step = [&](uint32_t t, TileAhead &A) {
+  for (uint32_t t = c0; t < c1; ++t) {
+    const uint32_t slot = (t - c0) % kRing;
+    const uint32_t *w = sh.data[slot];
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     stamp<DIAG>(kp, t, 5);
-    stage_commit(sh.data, A.q);
-    const uint64_t a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: wave-uniform
-    const uint64_t e1 = a1 & kMask48, na = a2 & 0xffffffull;
-    const bool reuse = tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && e1 == pos + 1;
-    if (reuse) {  // pass 1 walked this tile from the same (exact) entry: its offsets are the chain's
-      reinterpret_cast<uint32_t *>(sh.srec)[lane] = A.off0;
-      reinterpret_cast<uint32_t *>(sh.srec)[lane + 64] = A.off1;
+    const uint32_t ahead = c1 - 1 - t < (uint32_t)(kRing - 1) ? c1 - 1 - t : (uint32_t)(kRing - 1);
+    if (t + kRing - 1 < c1) {
+      const uint32_t ns = (slot + kRing - 1) % kRing;
+      dma_tile(kp, tile_lo + (uint64_t)(kRing - 1) * kTile, sh.data[ns]);
+      dma_extras(kp, t + kRing - 1, sh.off[ns], sh.agg[ns]);
     }
-    wave_sync();
-    if (t + 2 < c1) ahead_issue(kp, t + 2, A);
+    wait_dma<kDmaEmit>(ahead);
+    const uint32_t *ag = sh.agg[slot];
+    const uint64_t a1 = uni64((uint64_t)ag[2] | ((uint64_t)ag[3] << 32));
+    const uint64_t a2 = uni64((uint64_t)ag[4] | ((uint64_t)ag[5] << 32));
+    const bool reuse = tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && (a1 & kMask48) == pos + 1;
+    // the record offsets: pass 1's (same exact entry) or a walk from the exact position
+    const uint16_t *srec = reuse ? reinterpret_cast<const uint16_t *>(sh.off[slot]) : sh.srec;
     uint32_t n = 0;
     uint64_t ex = pos;
     if (pos >= tile_lo && pos < tile_hi) {
       if (reuse) {
-        n = (uint32_t)na;
+        n = (uint32_t)(a2 & 0xffffffull);
         if (n) {  // exit = just past the last record (the walk advances by whole records)
-          const uint32_t rl = __builtin_amdgcn_readfirstlane(sh.srec[n - 1]);
-          ex = tile_lo + rl + 16u + __builtin_amdgcn_readfirstlane(hdr(sh.data, rl, 2, kp.big));
+          const uint32_t rl = __builtin_amdgcn_readfirstlane(srec[n - 1]);
+          ex = tile_lo + rl + 16u + __builtin_amdgcn_readfirstlane(hdr(w, rl, 2, kp.big));
         }
       } else {
-        ex = walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n);
+        ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n);
         wave_sync();
         if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
       }
@@ -1037,14 +1084,13 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
     for (int s = 0; s < kRounds; ++s) {
       if ((uint32_t)s * 64u >= n) break;
       const uint32_t i = lane + (uint32_t)s * 64u;
+      const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
       FlowWords f;
-      bool ok = false;
-      uint32_t rel = 0;
-      if (i < n) {
-        rel = sh.srec[i];
+      const uint32_t rel = srec[i];
+      const uint32_t st = decode_rec<true>(kp, w, tile_lo, rel, f, valid);
+      const bool ok = st == NPR_FLOW_OK && valid;
+      if (valid && (kp.rec_status || kp.rec_off || kp.recs)) {
         const uint64_t p = tile_lo + rel;
-        const uint32_t st = decode_rec<true>(kp, sh.data, tile_lo, rel, f);
-        ok = st == NPR_FLOW_OK;
         const uint64_t idx = pcnt + i;
         if (idx < kp.rec_cap) {
           if (kp.rec_status) kp.rec_status[idx] = (uint8_t)st;
@@ -1053,8 +1099,8 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
             const bool big = kp.big;
             uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
             row[0] = p;
-            row[1] = (uint64_t)hdr(sh.data, rel, 0, big) | ((uint64_t)hdr(sh.data, rel, 1, big) << 32);
-            row[2] = (uint64_t)hdr(sh.data, rel, 2, big) | ((uint64_t)hdr(sh.data, rel, 3, big) << 32);
+            row[1] = (uint64_t)hdr(w, rel, 0, big) | ((uint64_t)hdr(w, rel, 1, big) << 32);
+            row[2] = (uint64_t)hdr(w, rel, 2, big) | ((uint64_t)hdr(w, rel, 3, big) << 32);
           }
         }
       }
@@ -1062,16 +1108,9 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
       if (ok && kp.flows) {
         const uint64_t fi = pok + okbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
         if (fi < kp.flow_cap) {
-          const uint64_t p = tile_lo + rel;
           const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
-          u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-          dst[0] = u32x4{f.d[0], f.d[1], f.d[2], f.d[3]};
-          dst[1] = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
-          if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) {
-            u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
-            d6[0] = u32x4{f.v6[0], f.v6[1], f.v6[2], f.v6[3]};
-            d6[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
-          }
+          put_flow(kp.flows + o * 8, f, tile_lo + rel);
+          if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.flows_v6 + o * 8, f);
         }
       }
       okbase += (uint32_t)__builtin_popcountll(bal);
@@ -1081,10 +1120,10 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
     pok += okbase;
     if (lane == 0) {
       const uint32_t ep = kp.epoch;
-      TileSlot *slot = kp.slots + t;
-      st_agent(&slot->p[0], gran(ep, pos));
-      st_agent(&slot->p[1], gran(ep, pcnt));
-      st_agent(&slot->p[2], gran(ep, pok));
+      TileSlot *slot_t = kp.slots + t;
+      st_agent(&slot_t->p[0], gran(ep, pos));
+      st_agent(&slot_t->p[1], gran(ep, pcnt));
+      st_agent(&slot_t->p[2], gran(ep, pok));
       if (t == kp.ntiles - 1) {
         uint32_t fl = 0;
         if ((kp.rec_off || kp.recs || kp.rec_status) && pcnt > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
@@ -1098,11 +1137,7 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
       }
     }
     stamp<DIAG>(kp, t, 7);
-    wave_sync();  // done with this tile's LDS before the next commit
-  };
-  for (uint32_t t = c0; t < c1; t += 2) {
-    step(t, A);
-    if (t + 1 < c1) step(t + 1, B);
+    wave_sync();  // done with this slot's LDS before it is refilled
   }
 }
 
@@ -1195,11 +1230,10 @@ __device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseSha
         }
       } else {  // pass 1 started this tile elsewhere: stage, walk from the exact position, decode
         if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
-        u32x4 q[kChunks];
-        stage_issue(kp, tile_lo, q);
-        stage_commit(sh.data, q);
+        dma_tile(kp, tile_lo, sh.data[0]);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a rare path, draining the prefetch too is fine
         wave_sync();
-        ex = uni64(walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n));
+        ex = uni64(walk_tile(kp, sh.data[0], sh.srec, tile_lo, tile_hi, pos, n));
         wave_sync();
         stamp<DIAG>(kp, t, 6);
         for (int s = 0; s < kRounds; ++s) {
@@ -1210,7 +1244,7 @@ __device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseSha
           uint32_t rel = 0;
           if (i < n) {
             rel = sh.srec[i];
-            ok = decode_rec<true>(kp, sh.data, tile_lo, rel, f) == NPR_FLOW_OK;
+            ok = decode_rec<true>(kp, sh.data[0], tile_lo, rel, f) == NPR_FLOW_OK;
           }
           const uint64_t bal = __ballot(ok);
           if (ok && kp.flows) {

@@ -14,6 +14,13 @@ for a, b, nm in ((0, 1, "entry"), (1, 2, "walk"), (2, 3, "count"), (3, 4, "pub+f
                  (6, 7, "decode+write"), (0, 4, "scan tile"), (5, 7, "emit tile")):
     d = us[:, b] - us[:, a]
     print(f"{nm:14s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+c0 = s[:, 8] != 0  # chunk-first tiles (stamps 8..12)
+if c0.any():
+    u = lambda k: (s[c0, k] - t0) / 100.0
+    for a, b, nm in ((8, 9, "emit prologue"), (9, 10, "emit prefix"), (11, 12, "scan arrive+fold")):
+        d = u(b) - u(a)
+        print(f"{nm:16s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+    print("emit chunk entry pct", np.percentile(u(8), [0, 10, 50, 90, 100]).round(2))
 for c, nm in ((0, "scan"), (5, "emit")):
     e = c + 2 if c == 5 else 4
     ts = np.linspace(us[:, c].min(), us[:, e].max(), 12)
