@@ -106,22 +106,24 @@ def main():
         ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
     torch.cuda.synchronize()
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # ONE event pair brackets the K launches on their stream (per-step events would add marker
+    # packets between launches: ~8 us of GPU time per step, scripts/launch_probe.py)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for i in range(args.steps):
-        ev[i][0].record(stream)
         ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
-        ev[i][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     sm = ws.check()
     assert sm.n_records == n and sm.n_flows == n
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
+    kern_ms = ev0.elapsed_time(ev1) / args.steps  # average launch (scan + emit) on the device
     if args.stats:
         import ctypes
         lib, h = ws.ctx.lib, ws.ctx.handle

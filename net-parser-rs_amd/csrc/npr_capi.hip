@@ -39,7 +39,7 @@ struct npr_ctx {
   DevBuf counters;         // arrival counters: cnt1[g] at word 2g, cnt2[h] at word 2h+1 (layout independent of the input)
   bool dirty = false;
   uint32_t grid_scan = 0, grid_emit = 0;  // persistent grids: CUs x resident workgroups per CU
-  bool light = false;                     // flows-only launches park flows in pass 1 (NPR_LIGHT=1)      // a launch timed out: counters may be non-zero -> clear before the next launch
+  bool light = true;  // flows-only launches park flows in pass 1 (NPR_OPT_PARK_FLOWS; env NPR_LIGHT=0 clears)
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -153,7 +153,7 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   const char *fz = getenv("NPR_FUSED");
   const bool fused = fz && strcmp(fz, "1") == 0;  // two launches unless NPR_FUSED=1 (measured faster)
   const char *lt = getenv("NPR_LIGHT");
-  c->light = lt && strcmp(lt, "1") == 0;
+  c->light = !(lt && strcmp(lt, "0") == 0);  // parked-flow mode unless NPR_LIGHT=0 (measured faster)
   int per_cu_scan = fused ? npr::fused_blocks_per_cu() : npr::scan_blocks_per_cu();
   int per_cu_emit = fused ? 0 : npr::emit_blocks_per_cu();
   if (const char *v = getenv("NPR_SCAN_PER_CU")) per_cu_scan = std::max(1, atoi(v));
@@ -180,6 +180,17 @@ void npr_ctx_destroy(npr_ctx *c) {
 }
 
 const char *npr_ctx_last_error(const npr_ctx *c) { return c ? c->err.c_str() : "null context"; }
+
+npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
+  if (!c) return NPR_ERR_ARG;
+  switch (option) {
+    case NPR_OPT_PARK_FLOWS:
+      c->light = value != 0;
+      return NPR_OK;
+    default:
+      return fail(c, NPR_ERR_ARG, "unknown option");
+  }
+}
 
 npr_status npr_ctx_set_stats(npr_ctx *c, int enable) {
   if (!c) return NPR_ERR_ARG;
@@ -275,7 +286,7 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
   if ((st = ensure(c, c->counters, counter_bytes(nt), true))) return st;
-  // light mode (flows only, opt-in with NPR_LIGHT=1): pass 1 parks the flows, pass 2 copies them
+  // light mode (flows only, NPR_OPT_PARK_FLOWS): pass 1 parks the flows, pass 2 copies them
   const bool light = c->light && !o->record_offsets && !o->records && !o->record_status;
   if (light) {
     if ((st = ensure(c, c->park, nt * npr::kMaxOk * 32, false))) return st;

@@ -12,20 +12,20 @@
 //     per-layer flow dispatch         src/flow/layer2/ethernet.rs:39-133, src/flow/layer3/*.rs
 //   flow::convert_records             src/flow/mod.rs:101-123 -> reverse-order compaction
 //
-// Design: one 256-thread workgroup per 16 KiB tile of the record stream.
-//   1. stage the tile (+256 B halo) into LDS with 16-B buffer loads (OOB -> 0);
-//   2. tile 0 starts at the exact first record; every other tile SPECULATES its first record
-//      start from header plausibility (a 3-header chain check, lane-parallel);
-//   3. wave 0 walks the record chain through the tile, 64 records per step when the lengths
-//      repeat (a ballot confirms the stride), one per step otherwise;
-//   4. every record is decoded (status only) to count Ok flows;
-//   5. the tile publishes its speculative aggregate {entry, exit, count, ok} and then looks
-//      back (64 predecessor tiles per poll) for an exact prefix.  Aggregates are combined with
-//      a chain-consistency monoid: a predecessor's exit must equal the successor's speculated
-//      entry.  Any mismatch is resolved by waiting for the exact prefix of the mismatching
-//      tile, which re-walks itself from the true entry — so results equal the serial chain;
-//   6. with the exact prefix the tile writes the dense record table / status and its Ok flows
-//      at their reverse-order (convert_records) positions.
+// Design: two persistent passes of ONE-WAVE workgroups over 4 KiB tiles; each
+// wave owns a contiguous run of tiles staged into its LDS ring by DMA (no workgroup barriers).
+//   pass 1 (scan_chunk): the entry of a run's first tile is SPECULATED from header plausibility
+//     (later tiles continue the wave's own chain); the wave walks the chain (stride speculation,
+//     up to 256 records per step), decodes every record's status, and publishes the tile's
+//     aggregate A = {entry, exit, records, Ok flows}; the last arrival of each 64-tile group
+//     (and 4096-tile block) folds the group aggregates G1 (G2);
+//   pass 2 (emit_chunk): the exact chain state before a run is start ⊕ G2 ⊕ G1 ⊕ A, folded
+//     with a chain-consistency monoid (an aggregate counts only if its speculated entry is
+//     where the chain really continues; a contradiction waits for the offending tile's exact
+//     prefix P, which its own wave publishes here); then every tile is decoded again from the
+//     exact position (reusing pass 1's record offsets when its entry was right) and its Ok
+//     flows are written straight to their reverse-order (convert_records) rows.
+// A wrong speculation costs a wait or a re-walk, never a wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -442,19 +442,14 @@ __device__ __forceinline__ LaneSeg load_agg(const ParseParams &kp, int lvl, int6
   return L;
 }
 
+// lane i <- lane i+1 (DPP wave_shl:1, no LDS round trip); lane 63 gets 0
 __device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1);
-  const uint32_t hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x130, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x130, 0xf, 0xf, false);
   return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, o);
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), o);
-    v += ((uint64_t)hi << 32) | lo;
-  }
-  return v;
-}
+// whole-wave sum (DPP reduction of the device library); every lane must be active
+extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
 
 // Fold lanes [lo .. 0] (ascending tile order = descending lane) into one segment.  Fast path:
 // every link consistent, no END, no pass-through, all valid -> two wave sums; otherwise the
@@ -468,8 +463,9 @@ __device__ Seg fold_window(const ParseParams &kp, const LaneSeg &L, int lo) {
   const bool lo_bad = lane == lo && !L.valid;
   Seg r;
   if (__ballot(bad || endc || lo_bad) == 0ull) {
-    r.cnt = wave_sum64(inr ? L.cnt : 0ull);
-    r.ok = wave_sum64(inr ? L.ok : 0ull);
+    // a window of <= 64 aggregates never counts 2^32 records (<= 64 blocks x 1M records)
+    r.cnt = __ockl_wfred_add_u32(inr ? (uint32_t)L.cnt : 0u);
+    r.ok = __ockl_wfred_add_u32(inr ? (uint32_t)L.ok : 0u);
     r.entry = rl64(L.entry, lo);
     r.exit = rl64(L.exit, 0);
     r.first = (int64_t)rl64((uint64_t)L.first, lo);
@@ -692,28 +688,6 @@ __device__ __forceinline__ void wave_sync() {
 }
 
 typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
-constexpr int kChunks = (kStage / 16 + kWave - 1) / kWave;  // 16-B staging loads per lane
-
-// Stage tile t ([tile_lo, tile_lo + kStage) clipped to the input) into registers: one buffer
-// descriptor whose range ends at the input end (or the stage end), so chunks past it read 0.
-__device__ __forceinline__ void stage_issue(const ParseParams &kp, uint64_t tile_lo, u32x4 (&q)[kChunks]) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t avail = kp.len > tile_lo ? kp.len - tile_lo : 0;
-  const uint32_t nbytes = avail < (uint64_t)kStage ? (uint32_t)avail : (uint32_t)kStage;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + tile_lo), 0, (int)((nbytes + 15u) & ~15u), 0x00020000);
-#pragma unroll
-  for (int i = 0; i < kChunks; ++i)
-    q[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((lane + 64u * (uint32_t)i) * 16u), 0, 0);
-}
-// The LDS stage holds kChunks full 1-KiB rows (>= kStage bytes): every chunk is stored
-// unconditionally; chunks past the input / the stage were loaded out of range and are 0.
-__device__ __forceinline__ void stage_commit(uint32_t *data, const u32x4 (&q)[kChunks]) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (int i = 0; i < kChunks; ++i) *reinterpret_cast<u32x4 *>(&data[(lane + 64u * (uint32_t)i) * 4]) = q[i];
-}
-
 // speculation context of this launch: ts_usec bound from the file magic, the first record's
 // ts_sec as a reference (both read once per wave)
 __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
@@ -798,8 +772,9 @@ __device__ __forceinline__ void dma_tile(const ParseParams &kp, uint64_t tile_lo
 // pass 2 extras: pass 1's record-offset pairs of tile t and its A granules (dwords 0..5), sc1
 __device__ __forceinline__ void dma_extras(const ParseParams &kp, uint32_t t, uint32_t *off, uint32_t *agg) {
   const uint32_t lane = threadIdx.x & 63u;
-  const __amdgpu_buffer_rsrc_t ro =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, kMaxRec * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ro =  // light mode has no offset scratch: an empty range reads nothing
+      __builtin_amdgcn_make_buffer_rsrc(kp.srec_g ? (void *)(kp.srec_g + (uint64_t)t * kMaxRec) : (void *)kp.slots, 0,
+                                        kp.srec_g ? kMaxRec * 2 : 0, 0x00020000);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)off, 4, lane * 4u, 0, 0, 16);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)(off + 64), 4, lane * 4u + 256u, 0, 0, 16);
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.slots + t), 0, 24, 0x00020000);
@@ -879,6 +854,7 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
     if (c0 + k < c1) dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
   const SpecCtx sc = spec_ctx(kp);
   uint64_t carry = kNone;  // exact continuation of the chain
+  uint64_t chunk_ok = 0;   // light mode: Ok flows parked so far in this chunk
   for (uint32_t t = c0; t < c1; ++t) {
     const uint32_t slot = (t - c0) % kRing;
     const uint32_t *w = sh.data[slot];
@@ -926,13 +902,10 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
       const uint32_t rel = sh.srec[i];
       const bool ok = decode_rec<LIGHT>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
       const uint64_t bal = __ballot(ok);
-      if (LIGHT && ok) {
-        const uint32_t r = okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-        if (r < (uint32_t)kMaxOk) {  // always: see kMaxOk
-          const uint64_t row = ((uint64_t)t * kMaxOk + r) * 8;
-          put_flow(kp.park + row, f, tile_lo + rel);
-          if (kp.park_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.park_v6 + row, f);
-        }
+      if (LIGHT && ok) {  // parked contiguously per chunk, in chain order (<= kMaxOk per tile)
+        const uint64_t row = ((uint64_t)c0 * kMaxOk + chunk_ok + okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull))) * 8;
+        put_flow(kp.park + row, f, tile_lo + rel);
+        if (kp.park_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.park_v6 + row, f);
       }
       okc += (uint32_t)__builtin_popcountll(bal);
     }
@@ -946,6 +919,7 @@ __device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &s
     }
     // the chain continues into the next tile unless it ended here (Q3) or nothing was found
     carry = uni64((entry != kNone && ex >= tile_hi) ? ex : kNone);
+    chunk_ok += okc;
     stamp<DIAG>(kp, t, 4);
     wave_sync();  // done with this slot's LDS before it is refilled
   }
@@ -1027,22 +1001,20 @@ __device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X, uint64_t &e
   return true;
 }
 
-template <bool DIAG>
-__device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
-  const uint32_t lane = threadIdx.x & 63u;
-  stamp<DIAG>(kp, c0, 8);
+__device__ __forceinline__ void emit_prologue(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
 #pragma unroll
   for (int k = 0; k < kRing - 1; ++k)
     if (c0 + k < c1) {
       dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
       dma_extras(kp, c0 + k, sh.off[k], sh.agg[k]);
     }
-  Seg X;
-  uint64_t entry0;
-  stamp<DIAG>(kp, c0, 9);
-  if (!prefix_of(kp, c0, X, entry0)) return;
-  stamp<DIAG>(kp, c0, 10);
-  uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
+}
+
+// Tiles [c0, c1) from the exact chain state (pos, pcnt, pok); emit_prologue has been issued.
+template <bool DIAG>
+__device__ void emit_tiles(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1, uint64_t pos,
+                           uint64_t pcnt, uint64_t pok, uint64_t entry0) {
+  const uint32_t lane = threadIdx.x & 63u;
   for (uint32_t t = c0; t < c1; ++t) {
     const uint32_t slot = (t - c0) % kRing;
     const uint32_t *w = sh.data[slot];
@@ -1059,7 +1031,7 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
     const uint32_t *ag = sh.agg[slot];
     const uint64_t a1 = uni64((uint64_t)ag[2] | ((uint64_t)ag[3] << 32));
     const uint64_t a2 = uni64((uint64_t)ag[4] | ((uint64_t)ag[5] << 32));
-    const bool reuse = tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && (a1 & kMask48) == pos + 1;
+    const bool reuse = kp.srec_g && tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && (a1 & kMask48) == pos + 1;
     // the record offsets: pass 1's (same exact entry) or a walk from the exact position
     const uint16_t *srec = reuse ? reinterpret_cast<const uint16_t *>(sh.off[slot]) : sh.srec;
     uint32_t n = 0;
@@ -1141,150 +1113,112 @@ __device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &s
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// pass 2, light mode (flows only): emit_light_chunk — ONE WAVE owns the tiles [c0, c1).
-//   Same exact prefix as emit_chunk; then per tile, when pass 1 started the tile at the exact
-//   chain position (the common case), its parked Ok flows are simply copied to their
-//   convert_records positions — no staging, no walk, no decode.  A tile pass 1 mis-speculated
-//   is staged, walked from the exact position and decoded here (the full path).
-// ---------------------------------------------------------------------------------------------
-struct ParkAhead {  // what light pass 2 prefetches for a tile
-  u32x4 r0, r1;     // parked flow row `lane`
-  u32x4 v0, v1;     // its IPv6 side row (when flows_v6)
-  uint64_t a0, a1, a2;
-};
-
-__device__ __forceinline__ void park_issue(const ParseParams &kp, uint32_t t, ParkAhead &P) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t row = (uint64_t)t * kMaxOk * 8;
-  // sc1 (aux 16): L2-served, never a stale L1 line from an earlier launch
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park + row), 0, kMaxOk * 32, 0x00020000);
-  P.r0 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 32u), 0, 16);
-  P.r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lane * 32u + 16u), 0, 16);
-  if (kp.flows_v6) {
-    const __amdgpu_buffer_rsrc_t r6 =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park_v6 + row), 0, kMaxOk * 32, 0x00020000);
-    P.v0 = __builtin_amdgcn_raw_buffer_load_b128(r6, (int)(lane * 32u), 0, 16);
-    P.v1 = __builtin_amdgcn_raw_buffer_load_b128(r6, (int)(lane * 32u + 16u), 0, 16);
-  }
-  P.a0 = ld_agent(&kp.slots[t].a[0]);
-  P.a1 = ld_agent(&kp.slots[t].a[1]);
-  P.a2 = ld_agent(&kp.slots[t].a[2]);
+template <bool DIAG>
+__device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
+  stamp<DIAG>(kp, c0, 8);
+  emit_prologue(kp, sh, c0, c1);
+  Seg X;
+  uint64_t entry0;
+  stamp<DIAG>(kp, c0, 9);
+  if (!prefix_of(kp, c0, X, entry0)) return;
+  stamp<DIAG>(kp, c0, 10);
+  emit_tiles<DIAG>(kp, sh, c0, c1, uni64(X.exit), uni64(X.cnt), uni64(X.ok), entry0);
 }
 
+// ---------------------------------------------------------------------------------------------
+// pass 2, light mode (flows only): emit_light_chunk — ONE WAVE owns the tiles [c0, c1).
+//   Pass 1 parked the chunk's Ok flows contiguously in chain order.  When the chunk's first tile
+//   started at the exact chain position (the norm), the whole chunk is exact up to a chain END,
+//   so pass 2 is: the exact prefix, the chunk's counts summed up to that END, and ONE contiguous
+//   reversed copy of the parked rows into convert_records order — no staging, walk or decode.
+//   A chunk that started elsewhere runs the full per-tile path (emit_tiles), which also
+//   publishes the exact prefixes P(t) a waiting fold may need.
+// ---------------------------------------------------------------------------------------------
 template <bool DIAG>
 __device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
   const uint32_t lane = threadIdx.x & 63u;
-  ParkAhead A, B;  // two tiles in flight (the loop is unrolled by two)
-  park_issue(kp, c0, A);
-  if (c0 + 1 < c1) park_issue(kp, c0 + 1, B);
   Seg X;
   uint64_t entry0;
+  stamp<DIAG>(kp, c0, 8);
+  stamp<DIAG>(kp, c0, 9);
   if (!prefix_of(kp, c0, X, entry0)) return;
-  uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);  // exact chain state entering tile t
-  auto step = [&](uint32_t t, ParkAhead &A) {
-    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    stamp<DIAG>(kp, t, 5);
-    const uint64_t a0 = rl64(A.a0, 0), a1 = rl64(A.a1, 0), a2 = rl64(A.a2, 0);  // one address: uniform
-    const uint32_t ep = kp.epoch;
-    const bool reuse = tagged(a0, ep) && tagged(a1, ep) && tagged(a2, ep) && (a1 & kMask48) == pos + 1;
-    uint32_t n = 0, okc = 0;
-    uint64_t ex = pos;
-    if (pos >= tile_lo && pos < tile_hi) {
-      if (reuse) {
-        n = (uint32_t)(a2 & 0xffffffull);
-        okc = (uint32_t)((a2 >> 24) & 0xffffffull);
-        ex = a0 & kMask48;
-        stamp<DIAG>(kp, t, 6);
-        if (kp.flows) {
-          if (lane < okc && pok + lane < kp.flow_cap) {
-            const uint64_t o = kp.flow_cap - 1 - (pok + lane);  // convert_records pops from the end
-            u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-            d[0] = A.r0;
-            d[1] = A.r1;
-            if (kp.flows_v6 && ((A.r1[2] >> 16) & NPR_FLOW_KIND_IPV6)) {
-              u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
-              d6[0] = A.v0;
-              d6[1] = A.v1;
-            }
-          }
-          if (okc > 64u) {  // rows 64.. (tiles of many small Ok records): straight copies
-            const uint32_t r = 64u + lane;
-            if (r < okc && pok + r < kp.flow_cap) {
-              const uint64_t src = ((uint64_t)t * kMaxOk + r) * 8;
-              const uint64_t o = kp.flow_cap - 1 - (pok + r);
-              const u32x4 *s = reinterpret_cast<const u32x4 *>(kp.park + src);
-              u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-              const u32x4 x0 = __builtin_nontemporal_load(s), x1 = __builtin_nontemporal_load(s + 1);
-              d[0] = x0;
-              d[1] = x1;
-              if (kp.flows_v6 && ((x1[2] >> 16) & NPR_FLOW_KIND_IPV6)) {
-                const u32x4 *s6 = reinterpret_cast<const u32x4 *>(kp.park_v6 + src);
-                u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
-                d6[0] = __builtin_nontemporal_load(s6);
-                d6[1] = __builtin_nontemporal_load(s6 + 1);
-              }
-            }
-          }
+  stamp<DIAG>(kp, c0, 10);
+  const uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);
+  const uint64_t lo0 = kp.org + (uint64_t)c0 * kTile;
+  bool valid = pos < lo0;  // the chain ended before this chunk: nothing here
+  uint64_t n = 0, k = 0, ex = pos;
+  if (!valid) {
+    bool live = true;  // the chunk's chain has not ended yet
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t b = c0; b < c1 && live; b += 64) {
+      const uint32_t cnt = c1 - b < 64u ? c1 - b : 64u;
+      uint64_t w0 = 0, w1 = 0, w2 = 0;
+      for (;;) {  // the chunk's own aggregates (pass 1 published them before this point)
+        if (lane < cnt) {
+          w0 = ld_agent(&kp.slots[b + lane].a[0]);
+          w1 = ld_agent(&kp.slots[b + lane].a[1]);
+          w2 = ld_agent(&kp.slots[b + lane].a[2]);
         }
-      } else {  // pass 1 started this tile elsewhere: stage, walk from the exact position, decode
-        if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
-        dma_tile(kp, tile_lo, sh.data[0]);
-        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): a rare path, draining the prefetch too is fine
-        wave_sync();
-        ex = uni64(walk_tile(kp, sh.data[0], sh.srec, tile_lo, tile_hi, pos, n));
-        wave_sync();
-        stamp<DIAG>(kp, t, 6);
-        for (int s = 0; s < kRounds; ++s) {
-          if ((uint32_t)s * 64u >= n) break;
-          const uint32_t i = lane + (uint32_t)s * 64u;
-          FlowWords f;
-          bool ok = false;
-          uint32_t rel = 0;
-          if (i < n) {
-            rel = sh.srec[i];
-            ok = decode_rec<true>(kp, sh.data[0], tile_lo, rel, f) == NPR_FLOW_OK;
-          }
-          const uint64_t bal = __ballot(ok);
-          if (ok && kp.flows) {
-            const uint64_t fi = pok + okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-            if (fi < kp.flow_cap) {
-              const uint64_t o = kp.flow_cap - 1 - fi;
-              put_flow(kp.flows + o * 8, f, tile_lo + rel);
-              if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.flows_v6 + o * 8, f);
-            }
-          }
-          okc += (uint32_t)__builtin_popcountll(bal);
+        const bool ok = lane >= cnt || (tagged(w0, kp.epoch) && tagged(w1, kp.epoch) && tagged(w2, kp.epoch));
+        if (__ballot(!ok) == 0ull) break;
+        if (!spin_ok(kp, t0)) return;
+      }
+      if (b == c0) valid = (rl64(w1, 0) & kMask48) == pos + 1;  // the chunk started at the exact position
+      if (!valid) break;
+      for (uint32_t j = 0; j < cnt; ++j) {  // uniform: sum up to (and including) a chain END
+        const uint64_t e = rl64(w0, (int)j) & kMask48, c = rl64(w2, (int)j) & kMask48;
+        n += c & 0xffffffull;
+        k += (c >> 24) & 0xffffffull;
+        ex = e;
+        if (e < tile_end(kp, (int64_t)(b + j))) {  // END (Q3): the rest of the capture is void
+          live = false;
+          break;
         }
-        wave_sync();  // done with the staged tile
       }
     }
-    if (t + 2 < c1) park_issue(kp, t + 2, A);
-    pos = uni64(ex);
-    pcnt += n;
-    pok += okc;
-    if (lane == 0) {
-      TileSlot *slot = kp.slots + t;
-      st_agent(&slot->p[0], gran(ep, pos));
-      st_agent(&slot->p[1], gran(ep, pcnt));
-      st_agent(&slot->p[2], gran(ep, pok));
-      if (t == kp.ntiles - 1) {
-        uint32_t fl = 0;
-        if (kp.flows && pok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
-        kp.summary->n_records = pcnt;
-        kp.summary->n_flows = pok;
-        kp.summary->consumed = pos;
-        kp.summary->flags = fl;
-        kp.summary->entry = entry0;
-        kp.summary->epoch = kp.epoch;
+  }
+  if (!valid) {  // mis-speculated run: decode it here from the exact position
+    if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
+    emit_prologue(kp, sh, c0, c1);
+    emit_tiles<DIAG>(kp, sh, c0, c1, pos, pcnt, pok, entry0);
+    return;
+  }
+  stamp<DIAG>(kp, c0, 11);
+  // ONE contiguous copy: parked row j -> flow row flow_cap-1-(pok+j) (convert_records order).
+  // Range-checked buffer accesses (rows past flow_cap are out of range: nothing written).  A plain
+  // two-loads-in-flight loop: the parked rows were just written by pass 1 and are still in L2 /
+  // MALL; deeper batching (4 rows per lane) measured 3x slower here (r21 A/B) — it thrashes them.
+  if (kp.flows && k) {
+    const uint64_t base = (uint64_t)c0 * kMaxOk;
+    const uint64_t kk = pok >= kp.flow_cap ? 0 : (k < kp.flow_cap - pok ? k : kp.flow_cap - pok);  // rows that fit
+    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park + base * 8), 0, (int)(kk * 32), 0x00020000);
+    // destination rows [flow_cap-pok-kk, flow_cap-pok): row j lands at (kk-1-j) in this window
+    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(kp.flows + (kp.flow_cap - pok - kk) * 8), 0, (int)(kk * 32), 0x00020000);
+    for (uint64_t j = lane; j < kk; j += 64) {
+      const u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(j * 32u), 0, 2);  // nt: read once
+      const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(j * 32u + 16u), 0, 2);
+      const uint32_t o = (uint32_t)(kk - 1 - j) * 32u;
+      __builtin_amdgcn_raw_buffer_store_b128(x0, dst, (int)o, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(x1, dst, (int)(o + 16u), 0, 0);
+      if (kp.flows_v6 && (x1[2] >> 16) & NPR_FLOW_KIND_IPV6) {  // IPv6 rows: their parked side row too
+        const u32x4 *s6 = reinterpret_cast<const u32x4 *>(kp.park_v6 + (base + j) * 8);
+        u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + (kp.flow_cap - 1 - (pok + j)) * 8);
+        d6[0] = s6[0], d6[1] = s6[1];
       }
     }
-    stamp<DIAG>(kp, t, 7);
-  };
-  for (uint32_t t = c0; t < c1; t += 2) {
-    step(t, A);
-    if (t + 1 < c1) step(t + 1, B);
+  }
+  stamp<DIAG>(kp, c0, 12);
+  if (c1 == kp.ntiles && lane == 0) {  // this run holds the capture's last tile
+    const uint64_t tot_rec = pcnt + n, tot_ok = pok + k;
+    uint32_t fl = 0;
+    if (kp.flows && tot_ok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
+    kp.summary->n_records = tot_rec;
+    kp.summary->n_flows = tot_ok;
+    kp.summary->consumed = ex;
+    kp.summary->flags = fl;
+    kp.summary->entry = entry0;
+    kp.summary->epoch = kp.epoch;
   }
 }
 

@@ -33,6 +33,7 @@ KIND_UDP = 0x2
 
 # npr_status
 OK, INCOMPLETE, FAILURE, CUSTOM = 0, 1, 2, 3
+OPT_PARK_FLOWS = 1  # npr_ctx_set_option: flows-only parses park flows in pass 1 (default on)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1
 
@@ -82,7 +83,7 @@ assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24
 # Every symbol include/npr.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "npr_version", "npr_abi_version", "npr_ctx_create", "npr_ctx_destroy", "npr_ctx_last_error",
-    "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps",
+    "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps", "npr_ctx_set_option",
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_check", "npr_dev_extract_flows",
@@ -100,6 +101,7 @@ _SIGNATURES = {
     "npr_ctx_last_error": (ctypes.c_char_p, [_vp]),
     "npr_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
     "npr_ctx_set_stats": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "npr_ctx_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
     "npr_ctx_read_stats": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     "npr_ctx_read_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "npr_global_header_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _c_size_p]),

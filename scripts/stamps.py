@@ -15,7 +15,15 @@ for a, b, nm in ((0, 1, "entry"), (1, 2, "walk"), (2, 3, "count"), (3, 4, "pub+f
     d = us[:, b] - us[:, a]
     print(f"{nm:14s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
 c0 = s[:, 8] != 0  # chunk-first tiles (stamps 8..12)
-if c0.any():
+light = c0.any() and not s[:, 5].any()  # light mode: no per-tile emit stamps
+if light:  # chunk stamps [8]=[9] emit start [10] prefix known [11] counts summed [12] copied
+    u = lambda k: (s[c0, k] - t0) / 100.0
+    print("light emit span us %.2f  gap us %.2f" % (u(12).max() - u(8).min(), u(8).min() - us[:, 4].max()))
+    for a, b, nm in ((9, 10, "emit prefix"), (10, 11, "sum counts"), (11, 12, "copy"), (8, 12, "emit chunk")):
+        d = u(b) - u(a)
+        print(f"{nm:16s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
+    print("emit chunk entry pct", np.percentile(u(8), [0, 10, 50, 90, 100]).round(2))
+elif c0.any():
     u = lambda k: (s[c0, k] - t0) / 100.0
     for a, b, nm in ((8, 9, "emit prologue"), (9, 10, "emit prefix"), (11, 12, "scan arrive+fold")):
         d = u(b) - u(a)

@@ -10,8 +10,6 @@ import json
 import os
 import struct
 
-os.environ.setdefault("NPR_LIGHT", "1")  # exercise the parked-flow mode in the flows_only cases
-
 import numpy as np
 import pytest
 import torch
@@ -36,9 +34,17 @@ def to_dev(blob):
 def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     """Run the device path on `blob` and compare everything with the oracle.
 
-    light=True requests flows only (no record table / status): the launch then runs in the
-    parked-flow mode (pass 1 parks each tile's Ok flows, pass 2 copies them), so the flow table,
-    counts and `consumed` are compared."""
+    light requests flows only (no record table / status), so the flow table, counts and
+    `consumed` are compared.  light=True runs the parked-flow mode (pass 1 parks each
+    tile's Ok flows, pass 2 reverses them: the default); light="decode" the same launch with
+    NPR_OPT_PARK_FLOWS off (pass 2 re-decodes the records)."""
+    if light == "decode":
+        ctx = npr.context(0)
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PARK_FLOWS, 0))
+        try:
+            return check_parity(blob, start, endianness, ws, light=True)
+        finally:
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PARK_FLOWS, 1))
     if start == 24:
         rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
         assert rc == 0
@@ -110,7 +116,7 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-LIGHT = pytest.mark.parametrize("light", [False, True], ids=["full", "flows_only"])
+LIGHT = pytest.mark.parametrize("light", [False, True, "decode"], ids=["full", "flows_only", "flows_only_decode"])
 
 
 @LIGHT
