@@ -34,12 +34,7 @@ struct npr_ctx {
   int stats_mode = 0;               // 2 = also per-tile phase stamps
   DevBuf stamps;
   uint64_t stamp_tiles = 0;
-  DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile (full mode)
-  DevBuf park, park_v6;    // pass-1 parked flows: kMaxOk 32-B rows per tile (light mode)
-  DevBuf counters;         // arrival counters: cnt1[g] at word 2g, cnt2[h] at word 2h+1 (layout independent of the input)
-  bool dirty = false;
-  uint32_t grid_scan = 0, grid_emit = 0;  // persistent grids: CUs x resident workgroups per CU
-  bool light = true;  // flows-only launches park flows in pass 1 (NPR_OPT_PARK_FLOWS; env NPR_LIGHT=0 clears)
+  DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -115,19 +110,24 @@ extern "C" {
 const char *npr_version(void) { return NPR_VERSION_STRING; }
 int npr_abi_version(void) { return NPR_ABI_VERSION; }
 
-static uint64_t ngroups1(uint64_t nt) { return (nt + npr::kGroup - 1) / npr::kGroup; }
-static uint64_t ngroups2(uint64_t nt) { return (ngroups1(nt) + npr::kGroup - 1) / npr::kGroup; }
-// tile slots, then G1 slots, then G2 slots: one allocation (granules are epoch-tagged, so the
+// elements per level: [0] tiles, [l] = ceil([l-1] / 64)
+static void level_sizes(uint64_t nt, uint64_t n[npr::kLevels + 1]) {
+  n[0] = nt;
+  for (int l = 1; l <= npr::kLevels; ++l) n[l] = (n[l - 1] + 63) / 64;
+}
+// tile slots, then the level-1..3 group slots: one allocation (granules are epoch-tagged, so the
 // layout may shift between launches)
 static uint64_t slot_bytes(uint64_t nt) {
-  return nt * sizeof(npr::TileSlot) + (ngroups1(nt) + ngroups2(nt)) * sizeof(npr::GroupSlot);
+  uint64_t n[npr::kLevels + 1];
+  level_sizes(nt, n);
+  uint64_t b = nt * sizeof(npr::TileSlot);
+  for (int l = 1; l <= npr::kLevels; ++l) b += n[l] * sizeof(npr::GroupSlot);
+  return b;
 }
-static uint64_t counter_bytes(uint64_t nt) { return (2 * ngroups1(nt) + 2) * sizeof(uint32_t); }
 
 uint64_t npr_workspace_bytes(uint64_t len) {
   const uint64_t nt = tiles_for(len, 0, nullptr);
-  // + the larger of the full-mode offset scratch and the light-mode parked flows (+ IPv6 rows)
-  return slot_bytes(nt) + counter_bytes(nt) + nt * std::max<uint64_t>(npr::kMaxRec * sizeof(uint16_t), 2 * npr::kMaxOk * 32);
+  return slot_bytes(nt) + nt * npr::kMaxRec * sizeof(uint16_t);  // + pass 1's record-offset scratch
 }
 
 npr_status npr_ctx_create(int device, npr_ctx **out) {
@@ -144,22 +144,6 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
-    npr_ctx_destroy(c);
-    return NPR_ERR_DEVICE;
-  }
-  // NPR_FUSED=1 selects the one-launch variant; NPR_*_PER_CU override occupancy
-  const char *fz = getenv("NPR_FUSED");
-  const bool fused = fz && strcmp(fz, "1") == 0;  // two launches unless NPR_FUSED=1 (measured faster)
-  const char *lt = getenv("NPR_LIGHT");
-  c->light = !(lt && strcmp(lt, "0") == 0);  // parked-flow mode unless NPR_LIGHT=0 (measured faster)
-  int per_cu_scan = fused ? npr::fused_blocks_per_cu() : npr::scan_blocks_per_cu();
-  int per_cu_emit = fused ? 0 : npr::emit_blocks_per_cu();
-  if (const char *v = getenv("NPR_SCAN_PER_CU")) per_cu_scan = std::max(1, atoi(v));
-  if (const char *v = getenv("NPR_EMIT_PER_CU"); v && !fused) per_cu_emit = std::max(1, atoi(v));
-  c->grid_scan = (uint32_t)(prop.multiProcessorCount * per_cu_scan);
-  c->grid_emit = (uint32_t)(prop.multiProcessorCount * per_cu_emit);
   *out = c;
   return NPR_OK;
 }
@@ -168,7 +152,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->slots, &c->srec, &c->park, &c->park_v6, &c->counters, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+  for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->scratch})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
@@ -184,8 +168,8 @@ const char *npr_ctx_last_error(const npr_ctx *c) { return c ? c->err.c_str() : "
 npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
   if (!c) return NPR_ERR_ARG;
   switch (option) {
-    case NPR_OPT_PARK_FLOWS:
-      c->light = value != 0;
+    case NPR_OPT_PARK_FLOWS:  // accepted for ABI 2 callers; one decode path since ABI 3
+      (void)value;
       return NPR_OK;
     default:
       return fail(c, NPR_ERR_ARG, "unknown option");
@@ -285,24 +269,12 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
-  if ((st = ensure(c, c->counters, counter_bytes(nt), true))) return st;
-  // light mode (flows only, NPR_OPT_PARK_FLOWS): pass 1 parks the flows, pass 2 copies them
-  const bool light = c->light && !o->record_offsets && !o->records && !o->record_status;
-  if (light) {
-    if ((st = ensure(c, c->park, nt * npr::kMaxOk * 32, false))) return st;
-    if (o->flows_v6 && (st = ensure(c, c->park_v6, nt * npr::kMaxOk * 32, false))) return st;
-  } else if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) {
-    return st;
-  }
+  if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
   hipStream_t s = pick(c, stream);
   if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
     c->epoch = 1;
     HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
     HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, 64, s));
-  }
-  if (c->dirty) {  // the previous launch aborted part-way: arrival counters are stale
-    HIP_CHECK(c, hipMemsetAsync(c->counters.p, 0, c->counters.cap, s));
-    c->dirty = false;
   }
   npr::ParseParams p{};
   p.buf = (const uint8_t *)input;
@@ -320,16 +292,17 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   if (speculative_start) p.flags |= npr::kFlagSpecStart;
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
-  p.ngroups1 = (uint32_t)ngroups1(nt);
-  p.ngroups2 = (uint32_t)ngroups2(nt);
-  p.groups1 = (npr::GroupSlot *)((char *)c->slots.p + nt * sizeof(npr::TileSlot));
-  p.groups2 = p.groups1 + p.ngroups1;
-  p.cnt1 = (uint32_t *)c->counters.p;      // word 2g
-  p.cnt2 = (uint32_t *)c->counters.p + 1;  // word 2h + 1
-  p.srec_g = light ? nullptr : (uint16_t *)c->srec.p;
-  p.park = light ? (uint32_t *)c->park.p : nullptr;
-  p.park_v6 = light && o->flows_v6 ? (uint32_t *)c->park_v6.p : nullptr;
-  if (light) p.flags |= npr::kFlagLight;
+  uint64_t nl[npr::kLevels + 1];
+  level_sizes(nt, nl);
+  npr::GroupSlot *gs = (npr::GroupSlot *)((char *)c->slots.p + nt * sizeof(npr::TileSlot));
+  p.ngroups[0] = (uint32_t)nt;
+  p.groups[0] = nullptr;
+  for (int l = 1; l <= npr::kLevels; ++l) {
+    p.groups[l] = gs;
+    p.ngroups[l] = (uint32_t)nl[l];
+    gs += nl[l];
+  }
+  p.srec_g = (uint16_t *)c->srec.p;
   p.abort_word = c->abort_word;
   p.rec_off = o->record_offsets;
   p.recs = o->records;
@@ -346,7 +319,7 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
     p.stamps = (uint64_t *)c->stamps.p;
     c->stamp_tiles = nt;
   }
-  HIP_CHECK(c, npr::launch_parse_extract(p, c->grid_scan, c->grid_emit, s));
+  HIP_CHECK(c, npr::launch_parse_extract(p, s));
   return NPR_OK;
 }
 
@@ -357,7 +330,6 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   HIP_CHECK(c, hipStreamSynchronize(s));
   if (hs) *hs = *c->summary_h;
   if (c->summary_h->epoch != c->epoch) {
-    c->dirty = true;
     return fail(c, NPR_ERR_TIMEOUT, "parse did not complete (tile hand-off timed out)");
   }
   if (c->summary_h->flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded (flags=%u)", c->summary_h->flags);

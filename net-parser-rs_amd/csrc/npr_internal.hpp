@@ -20,35 +20,41 @@ constexpr int kHalo = 128;             // bytes staged past the tile (headers + 
 constexpr int kStage = kTile + kHalo;  // bytes staged in LDS per tile
 constexpr int kMaxRec = kTile / 16;    // every record is >= 16 B
 constexpr int kRounds = kMaxRec / kWave;  // decode rounds of 64 records
-// An Ok record spans >= 16 + 42 bytes (header + Ethernet/IPv4/UDP), so at most this many Ok
-// records start in one tile: the per-tile capacity of the parked-flow scratch.
-constexpr int kMaxOk = (kTile + 57) / 58 + 1;
+static_assert(kTile % 1024 == 0 && kMaxRec % 128 == 0, "tile geometry");
 
-// Per-tile hand-off slot: A = speculative aggregate (k_scan_tiles), P = exact inclusive prefix
-// (k_emit_tiles).  Each word is an 8-byte {tag:16 | value:48} granule written by ONE
-// agent-scope store (self-validating: tag = the launch epoch).
-struct alignas(64) TileSlot {
-  uint64_t a[4];
-  uint64_t p[4];
+// Hand-off words are 8-byte {tag:16 | value:48} granules, each written by ONE agent-scope store
+// (self-validating: tag = the launch epoch).
+//
+// Per-tile slot.  a = the tile's speculative aggregate A (pass 1, by the tile's own wave);
+// e = the tile's exclusive prefix inside its 64-tile group (pass 1, by the group's folder);
+// p = the exact inclusive prefix P through the tile (pass 2, by the tile's own wave).
+struct alignas(128) TileSlot {
+  uint64_t a[3];  // {exit, entry + 1, n | okc << 24}
+  uint64_t e[5];  // prefix words, see kPre*
+  uint64_t p[3];  // {exit, cnt, ok}
+  uint64_t pad[5];
 };
-
-// Aggregates of 64 tiles (G1) and of 64 G1s = 4096 tiles (G2), folded by the last arriver.
-constexpr int kGroup = 64;
-struct alignas(32) GroupSlot {
-  uint64_t g[4];
+// Aggregates of 64 tiles (level 1), 64 level-1 groups (level 2) and 64 level-2 blocks (level 3),
+// each with its exclusive prefix inside its parent.
+struct alignas(128) GroupSlot {
+  uint64_t g[5];  // {exit, entry + 1, cnt, ok | valid << 32, mism + 1}
+  uint64_t e[5];  // prefix words, see kPre*
+  uint64_t pad[6];
 };
+// exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
+enum : int { kPreExit = 0, kPreCnt = 1, kPreOk = 2, kPreMism = 3, kPreEntry = 4 };
+constexpr int kLevels = 3;  // group levels above the tiles
 
 enum : uint32_t {
   kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
-  kFlagLight = 4u,        // flows only (no record table / status): pass 1 parks the flows, pass 2 copies
   kFlagSpecStart = 8u,    // `start` is not a known record boundary: speculate tile 0's entry too
 };
 
 // optional diagnostic counters (ParseParams::stats, NULL in production launches)
 enum : uint32_t {
   kStatRewalk = 0,     // tiles pass 2 re-walked (pass 1's entry was not the exact one)
-  kStatMismWait = 1,   // prefix folds that waited for a mis-speculated tile's exact prefix
-  kStatWeakEntry = 4,  // tiles that used a weak speculation
+  kStatMismWait = 1,   // prefixes that waited for a mis-speculated tile's exact prefix
+  kStatFoldSlow = 2,   // pass-1 group folds that took the serial (inconsistent-link) path
   kStatNoEntry = 5,    // tiles with no plausible record start
   kStatCount = 8
 };
@@ -68,13 +74,9 @@ struct ParseParams {
   uint32_t flags;
   uint32_t timeout_ticks;  // s_memrealtime (100 MHz) ticks before a stalled hand-off aborts
   TileSlot *slots;
-  GroupSlot *groups1;      // ngroups1 = ceil(ntiles / 64)
-  GroupSlot *groups2;      // ceil(ngroups1 / 64)
-  uint32_t *cnt1, *cnt2;   // arrival counters (zero between launches)
-  uint32_t ngroups1, ngroups2;
+  GroupSlot *groups[kLevels + 1];  // [1..3]; [0] unused
+  uint32_t ngroups[kLevels + 1];   // [0] = ntiles, [l] = ceil(ngroups[l-1] / 64)
   uint16_t *srec_g;        // pass-1 record offsets, kMaxRec per tile (pass 2 reuses them)
-  uint32_t *park;          // light mode: pass-1 Ok flows, kMaxOk 32-B rows per tile
-  uint32_t *park_v6;       // light mode: their IPv6 addresses (when flows_v6)
   uint32_t *abort_word;    // == epoch once any tile aborted
   uint64_t *rec_off;
   npr_record *recs;
@@ -85,16 +87,11 @@ struct ParseParams {
   uint64_t flow_cap;
   npr_summary *summary;
   uint32_t *stats;         // kStatCount counters or NULL
-  uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][8] or NULL
+  uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][kStampWords] or NULL
 };
 
-// Persistent grids (capped at ntiles) whose workgroups each own a contiguous run of tiles:
-// grid_emit == 0 -> one fused launch (k_parse_fused, grid_scan workgroups); else k_scan_tiles
-// then k_emit_tiles.
-hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s);
-int scan_blocks_per_cu();  // resident workgroups per CU (occupancy API)
-int emit_blocks_per_cu();
-int fused_blocks_per_cu();
+// k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each.
+hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);

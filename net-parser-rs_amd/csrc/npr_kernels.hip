@@ -1,30 +1,30 @@
 // npr_kernels.hip — CDNA4 (gfx950) kernels for the pcap record chain + flow extraction.
 //
 // Replaces, on the device, the nom parse paths of protectwise/net-parser-rs 0.3.0:
-//   PcapRecords::parse loop           src/record.rs:21-54     -> walk_tile() + decoupled look-back
+//   PcapRecords::parse loop           src/record.rs:21-54     -> walk_tile() + speculation + prefix folds
 //   PcapRecord::parse                 src/record.rs:102-121   -> hdr() / walk_tile()
-//   FlowExtraction::extract_flow      src/flow/mod.rs:20-48   -> decode<>()
+//   FlowExtraction::extract_flow      src/flow/mod.rs:20-48   -> decode<>() / decode_fast<>()
 //     Ethernet::parse + vlan loop     src/layer2/ethernet.rs:143-216
 //     IPv4::parse / parse_ipv4        src/layer3/ipv4.rs:76-160
 //     IPv6::parse / parse_next_header src/layer3/ipv6.rs:29-99
 //     Arp::parse                      src/layer3/arp.rs:54-76
 //     Tcp::parse / Udp::parse         src/layer4/tcp.rs:59-101, src/layer4/udp.rs:33-50
 //     per-layer flow dispatch         src/flow/layer2/ethernet.rs:39-133, src/flow/layer3/*.rs
-//   flow::convert_records             src/flow/mod.rs:101-123 -> reverse-order compaction
+//   flow::convert_records             src/flow/mod.rs:101-123 -> reverse-order rows, ranked by ballot
 //
-// Design: two persistent passes of ONE-WAVE workgroups over 4 KiB tiles; each
-// wave owns a contiguous run of tiles staged into its LDS ring by DMA (no workgroup barriers).
-//   pass 1 (scan_chunk): the entry of a run's first tile is SPECULATED from header plausibility
-//     (later tiles continue the wave's own chain); the wave walks the chain (stride speculation,
-//     up to 256 records per step), decodes every record's status, and publishes the tile's
-//     aggregate A = {entry, exit, records, Ok flows}; the last arrival of each 64-tile group
-//     (and 4096-tile block) folds the group aggregates G1 (G2);
-//   pass 2 (emit_chunk): the exact chain state before a run is start ⊕ G2 ⊕ G1 ⊕ A, folded
-//     with a chain-consistency monoid (an aggregate counts only if its speculated entry is
-//     where the chain really continues; a contradiction waits for the offending tile's exact
-//     prefix P, which its own wave publishes here); then every tile is decoded again from the
-//     exact position (reusing pass 1's record offsets when its entry was right) and its Ok
-//     flows are written straight to their reverse-order (convert_records) rows.
+// Design: two streaming passes of ONE-WAVE workgroups, one per 4 KiB tile, each
+// tile staged into LDS by DMA (no workgroup barriers, no waits on other tiles in the common case).
+//   pass 1 (k_count_tiles): a tile's entry is SPECULATED from header plausibility (tile 0 starts
+//     at `start`); the wave walks the chain (stride speculation, up to 256 records per step),
+//     decodes every record's status and publishes A = {entry, exit, records, Ok flows}.  The
+//     wave that finishes a group's last tile folds the group (64 tiles, then 64 groups, then 64
+//     blocks) with a chain-consistency monoid: the group's aggregate and every member's
+//     exclusive prefix inside it;
+//   pass 2 (k_emit_tiles): the exact chain state before a tile is the anchor folded with its
+//     three exclusive prefixes (point loads issued beside the tile's DMA); a contradiction waits
+//     for the offending tile's exact prefix P, which its own wave publishes in this pass; every
+//     record is decoded from the exact position (reusing pass 1's offsets when its entry was
+//     right) and its Ok flow goes straight to its reverse-order (convert_records) row.
 // A wrong speculation costs a wait or a re-walk, never a wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -336,7 +336,6 @@ __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint
   }
   return st;
 }
-
 // ---------------------------------------------------------------------------------------------
 // hand-off granules (MI355X_MICROARCH.md "R2": the data IS the flag, {tag, value} 8-B)
 // ---------------------------------------------------------------------------------------------
@@ -359,7 +358,8 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
   return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
-// A segment of consecutive tiles [first, last] under speculation.
+// A segment of consecutive tiles [first, last] under speculation: the chain entered at `entry`
+// (speculated) and left at `exit`, with `cnt` records and `ok` Ok flows in between.
 struct Seg {
   uint64_t entry, exit, cnt, ok;
   int64_t first, last, mism;  // mism: lowest tile whose speculated entry is contradicted
@@ -403,29 +403,36 @@ __device__ __forceinline__ bool spin_ok(const ParseParams &kp, uint64_t t0) {
   return true;
 }
 
-// One lane's element of a 64-wide fold: a tile aggregate (level 0), a 64-tile group aggregate
-// (level 1) or a 4096-tile block aggregate (level 2).
+// Elements of level l: tiles (l = 0) and groups of 64^l tiles (l = 1..kLevels).
+__device__ __forceinline__ int64_t elem_first(int lvl, int64_t idx) { return idx << (6 * lvl); }
+__device__ __forceinline__ int64_t elem_last(const ParseParams &kp, int lvl, int64_t idx) {
+  const int64_t l = ((idx + 1) << (6 * lvl)) - 1;
+  return l < (int64_t)kp.ntiles - 1 ? l : (int64_t)kp.ntiles - 1;
+}
+__device__ __forceinline__ uint64_t *prefix_words(const ParseParams &kp, int lvl, int64_t idx) {
+  return lvl == 0 ? kp.slots[idx].e : kp.groups[lvl][idx].e;
+}
+
+// One lane's element of a 64-wide window of aggregates.
 struct LaneSeg {
   uint64_t entry, exit, cnt, ok;
   int64_t first, last, mism;
   bool valid, present;
 };
 
-// level 0: A = {exit, entry + 1, n | okc << 24};  levels 1/2: {exit, entry + 1, cnt, ok | valid << 32 | mism_rel << 33}
+// level 0: A = {exit, entry + 1, n | okc << 24};  levels 1..3: G = {exit, entry + 1, cnt, ok | valid << 32, mism + 1}
 __device__ __forceinline__ LaneSeg load_agg(const ParseParams &kp, int lvl, int64_t idx, bool inr) {
   LaneSeg L{};
   L.mism = -1;
   L.valid = true;
-  const int sh = 6 * lvl;
-  L.first = idx << sh;
-  const int64_t last = ((idx + 1) << sh) - 1;
-  L.last = last < (int64_t)kp.ntiles - 1 ? last : (int64_t)kp.ntiles - 1;
+  L.first = elem_first(lvl, idx);
+  L.last = elem_last(kp, lvl, idx);
   if (!inr) return L;
   const uint32_t ep = kp.epoch;
-  const uint64_t *w = lvl == 0 ? kp.slots[idx].a : (lvl == 1 ? kp.groups1[idx].g : kp.groups2[idx].g);
+  const uint64_t *w = lvl == 0 ? kp.slots[idx].a : kp.groups[lvl][idx].g;
   const uint64_t w0 = ld_agent(w + 0), w1 = ld_agent(w + 1), w2 = ld_agent(w + 2);
-  const uint64_t w3 = lvl == 0 ? w0 : ld_agent(w + 3);
-  L.present = tagged(w0, ep) && tagged(w1, ep) && tagged(w2, ep) && tagged(w3, ep);
+  const uint64_t w3 = lvl == 0 ? w0 : ld_agent(w + 3), w4 = lvl == 0 ? w0 : ld_agent(w + 4);
+  L.present = tagged(w0, ep) && tagged(w1, ep) && tagged(w2, ep) && tagged(w3, ep) && tagged(w4, ep);
   const uint64_t e1 = w1 & kMask48;
   L.entry = e1 ? e1 - 1 : kNone;
   L.exit = w0 & kMask48;
@@ -433,13 +440,51 @@ __device__ __forceinline__ LaneSeg load_agg(const ParseParams &kp, int lvl, int6
     L.cnt = w2 & 0xffffffull;
     L.ok = (w2 >> 24) & 0xffffffull;
   } else {
-    const uint64_t v3 = w3 & kMask48;
+    const uint64_t v3 = w3 & kMask48, m = w4 & kMask48;
     L.cnt = w2 & kMask48;
     L.ok = v3 & 0xffffffffull;
     L.valid = (v3 >> 32) & 1ull;
-    L.mism = L.valid ? -1 : L.first + (int64_t)((v3 >> 33) & 0x7fffull);
+    L.mism = L.valid ? -1 : (int64_t)m - 1;
   }
   return L;
+}
+
+__device__ __forceinline__ void put_agg(const ParseParams &kp, GroupSlot *G, const Seg &c) {
+  const uint32_t ep = kp.epoch;
+  st_agent(&G->g[0], gran(ep, c.exit));
+  st_agent(&G->g[1], gran(ep, c.entry == kNone ? 0ull : c.entry + 1));
+  st_agent(&G->g[2], gran(ep, c.cnt));
+  st_agent(&G->g[3], gran(ep, (c.ok & 0xffffffffull) | ((uint64_t)c.valid << 32)));
+  st_agent(&G->g[4], gran(ep, c.valid ? 0ull : (uint64_t)c.mism + 1));
+}
+
+// exclusive prefix of an element inside its parent: {exit, cnt, ok | valid << 32 | empty << 33,
+// mism + 1, entry + 1} (a parent's first child has the empty prefix)
+__device__ __forceinline__ void put_prefix(const ParseParams &kp, uint64_t *e, const Seg &p, bool empty) {
+  const uint32_t ep = kp.epoch;
+  st_agent(e + kPreExit, gran(ep, empty ? 0ull : p.exit));
+  st_agent(e + kPreCnt, gran(ep, empty ? 0ull : p.cnt));
+  st_agent(e + kPreOk, gran(ep, empty ? (1ull << 32) | (1ull << 33) : (p.ok & 0xffffffffull) | ((uint64_t)p.valid << 32)));
+  st_agent(e + kPreMism, gran(ep, (empty || p.valid) ? 0ull : (uint64_t)p.mism + 1));
+  st_agent(e + kPreEntry, gran(ep, (empty || p.entry == kNone) ? 0ull : p.entry + 1));
+}
+
+// the prefix words of element idx of level lvl (already loaded) as a segment of tiles
+// [first tile of the parent, first tile of the element - 1]
+__device__ __forceinline__ Seg prefix_seg(uint64_t e0, uint64_t e1, uint64_t e2, uint64_t e3, uint64_t e4, int lvl,
+                                          int64_t idx, bool &empty) {
+  Seg s;
+  const uint64_t v = e2 & kMask48, m = e3 & kMask48, en = e4 & kMask48;
+  s.exit = e0 & kMask48;
+  s.cnt = e1 & kMask48;
+  s.ok = v & 0xffffffffull;
+  s.valid = (v >> 32) & 1ull;
+  empty = (v >> 33) & 1ull;
+  s.mism = s.valid ? -1 : (int64_t)m - 1;
+  s.entry = en ? en - 1 : kNone;
+  s.first = elem_first(lvl, idx & ~63ll);
+  s.last = elem_first(lvl, idx) - 1;
+  return s;
 }
 
 // lane i <- lane i+1 (DPP wave_shl:1, no LDS round trip); lane 63 gets 0
@@ -447,6 +492,24 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
   const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x130, 0xf, 0xf, false);
   const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x130, 0xf, 0xf, false);
   return ((uint64_t)hi << 32) | lo;
+}
+// lane i <- lane i-1 (lane 0 gets lane 63's value; callers ignore it)
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
+  const int src = ((int)(threadIdx.x & 63u) + 63) & 63;
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+  const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+// exclusive prefix sum over the 64 lanes (every lane active)
+__device__ __forceinline__ uint32_t excl_scan_u32(uint32_t v) {
+  const int lane = (int)(threadIdx.x & 63u);
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
+    if (lane >= o) x += y;
+  }
+  return x - v;
 }
 // whole-wave sum (DPP reduction of the device library); every lane must be active
 extern "C" __device__ uint32_t __ockl_wfred_add_u32(uint32_t);
@@ -526,6 +589,41 @@ __device__ bool wait_exact(const ParseParams &kp, int64_t m, Seg &X, uint64_t t0
   }
 }
 
+// Generic exact prefix of tiles [a, t) continuing X: ascending, largest aligned aggregates
+// first; every contradiction is settled by the exact prefix of the offending tile (published by
+// its own wave in k_emit_tiles; that wave was dispatched earlier, so it is resident or done).
+template <bool DIAG>
+__device__ bool prefix_generic(const ParseParams &kp, Seg X, int64_t a, int64_t t, Seg &out, uint64_t t0) {
+  for (;;) {
+    if (!X.valid) {
+      const int64_t m = X.mism;
+      if (!wait_exact(kp, m, X, t0)) return false;
+      if (DIAG && kp.stats && (threadIdx.x & 63u) == 0) atomicAdd(kp.stats + kStatMismWait, 1u);
+      a = m + 1;
+    }
+    if (a >= t) break;
+    int lvl = 0;
+    for (int l = kLevels; l >= 1; --l) {
+      const int64_t span = 1ll << (6 * l);
+      if ((a & (span - 1)) == 0 && t - a >= span) {
+        lvl = l;
+        break;
+      }
+    }
+    const int64_t unit = 1ll << (6 * lvl);
+    int64_t cnt = (t - a) >> (6 * lvl);
+    const int64_t to_parent = lvl == kLevels ? 64 : ((unit << 6) - (a & ((unit << 6) - 1))) >> (6 * lvl);
+    cnt = cnt < to_parent ? cnt : to_parent;
+    cnt = cnt < 64 ? cnt : 64;
+    Seg Y;
+    if (!fold_range(kp, lvl, a >> (6 * lvl), (int)cnt, Y, t0)) return false;
+    X = combine(kp, X, Y);
+    a += cnt << (6 * lvl);
+  }
+  out = X;
+  return true;
+}
+
 __device__ __forceinline__ Seg start_seg(const ParseParams &kp) {
   Seg X;
   X.entry = X.exit = kp.start;
@@ -536,40 +634,69 @@ __device__ __forceinline__ Seg start_seg(const ParseParams &kp) {
   return X;
 }
 
-// Generic exact prefix of tiles [a, t) continuing X (wave 0): ascending, largest aligned
-// aggregates first; every contradiction is settled by the exact prefix of the offending tile.
-__device__ bool prefix_generic(const ParseParams &kp, Seg X, int64_t a, int64_t t, Seg &out, uint64_t t0) {
+// Fold element `idx` of level `lvl` (1..kLevels) from its (up to 64) children of level lvl-1:
+// publish the element's aggregate G and every child's exclusive prefix inside the element.  Run
+// by the wave that produced the element's LAST child; the other children come from waves
+// dispatched before it.  False if a wait timed out (the launch then reports NPR_ERR_TIMEOUT).
+template <bool DIAG>
+__device__ bool fold_children(const ParseParams &kp, int lvl, int64_t idx, uint64_t t0) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const int64_t c0 = idx << 6;
+  const int64_t nch = (int64_t)kp.ngroups[lvl - 1];
+  const int size = (int)(nch - c0 < 64 ? nch - c0 : 64);
+  const bool inr = lane < size;
+  LaneSeg L;
   for (;;) {
-    if (!X.valid) {
-      const int64_t m = X.mism;
-      if (!wait_exact(kp, m, X, t0)) return false;
-      if (kp.stats && (threadIdx.x & 63u) == 0) atomicAdd(kp.stats + kStatMismWait, 1u);
-      a = m + 1;
-    }
-    if (a >= t) break;
-    int lvl;
-    int64_t cnt;
-    if ((a & 4095) == 0 && t - a >= 4096) {
-      lvl = 2;
-      cnt = (t - a) >> 12;
-    } else if ((a & 63) == 0 && t - a >= 64) {
-      lvl = 1;
-      cnt = (t - a) >> 6;
-      const int64_t to_blk = (4096 - (a & 4095)) >> 6;
-      cnt = cnt < to_blk ? cnt : to_blk;
-    } else {
-      lvl = 0;
-      cnt = t - a;
-      const int64_t to_grp = 64 - (a & 63);
-      cnt = cnt < to_grp ? cnt : to_grp;
-    }
-    cnt = cnt < 64 ? cnt : 64;
-    Seg Y;
-    if (!fold_range(kp, lvl, a >> (6 * lvl), (int)cnt, Y, t0)) return false;
-    X = combine(kp, X, Y);
-    a += cnt << (6 * lvl);
+    L = load_agg(kp, lvl - 1, c0 + lane, inr);
+    if (__ballot(inr && !L.present) == 0ull) break;
+    if (!spin_ok(kp, t0)) return false;
   }
-  out = X;
+  const uint64_t prev_exit = shfl_up64(L.exit);  // lane j <- lane j-1
+  const bool link_bad = inr && (!L.valid || (lane > 0 && L.entry != prev_exit));
+  const bool end_mid = lane < size - 1 && L.exit < tile_end(kp, L.last);
+  Seg ep{}, agg;
+  if (__ballot(link_bad || end_mid) == 0ull) {
+    // consistent chain through every child: exclusive prefixes are plain prefix sums
+    const uint32_t c = inr ? (uint32_t)L.cnt : 0u, o = inr ? (uint32_t)L.ok : 0u;
+    const uint32_t cx = excl_scan_u32(c), ox = excl_scan_u32(o);
+    ep.entry = rl64(L.entry, 0);
+    ep.exit = prev_exit;
+    ep.cnt = cx;
+    ep.ok = ox;
+    ep.valid = true;
+    ep.mism = -1;
+    agg.entry = ep.entry;
+    agg.exit = rl64(L.exit, size - 1);
+    agg.cnt = (uint32_t)__builtin_amdgcn_readlane((int)(cx + c), size - 1);
+    agg.ok = (uint32_t)__builtin_amdgcn_readlane((int)(ox + o), size - 1);
+    agg.valid = true;
+    agg.mism = -1;
+  } else {
+    // the serial monoid (wave-uniform): an END, a pass-through or a mis-speculated child
+    if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatFoldSlow, 1u);
+    const uint64_t bval = __ballot(L.valid);
+    Seg r{};
+    for (int j = 0; j < size; ++j) {
+      Seg y;
+      y.entry = rl64(L.entry, j);
+      y.exit = rl64(L.exit, j);
+      y.cnt = rl64(L.cnt, j);
+      y.ok = rl64(L.ok, j);
+      y.first = (int64_t)rl64((uint64_t)L.first, j);
+      y.last = (int64_t)rl64((uint64_t)L.last, j);
+      y.mism = (int64_t)rl64((uint64_t)L.mism, j);
+      y.valid = (bval >> j) & 1ull;
+      if (j == 0) {
+        r = y;
+      } else {
+        if (lane == j) ep = r;
+        r = combine(kp, r, y);
+      }
+    }
+    agg = r;
+  }
+  if (inr) put_prefix(kp, prefix_words(kp, lvl - 1, c0 + lane), ep, lane == 0);
+  if (lane == 0) put_agg(kp, kp.groups[lvl] + idx, agg);
   return true;
 }
 
@@ -591,15 +718,31 @@ __device__ __forceinline__ bool plaus(const SpecCtx &c, uint32_t ts, uint32_t fr
          (!c.has_ref || ts - c.ts_ref + kTsRefWindow <= 2u * kTsRefWindow);
 }
 
-// How plausible is LDS offset r as a record start?  0 = no; 1 = weak (its header passes but
-// fewer than two chained headers could be checked inside the staged window); 2 = strong.
-// A heuristic only: k_emit_tiles verifies every guess; a wrong one costs a wait, never a result.
-__device__ __forceinline__ int grade(const SpecCtx &c, const uint32_t *w, uint32_t r) {
-  if (c.avail - r < 16) return 0;
-  uint32_t ts = hdr(w, r, 0, c.big);
-  const uint32_t incl = hdr(w, r, 2, c.big);
-  if (!plaus(c, ts, hdr(w, r, 1, c.big), incl, hdr(w, r, 3, c.big))) return 0;
-  if (c.avail - r - 16 < incl) return 0;
+// The 16-B header at LDS offset r, in the capture's endianness: five aligned dword reads +
+// four v_alignbyte (every lane its own r).
+__device__ __forceinline__ void hdr4(const uint32_t *w, uint32_t r, bool big, uint32_t (&h)[4]) {
+  const uint32_t *p = w + (r >> 2);
+  const uint32_t sh = r & 3u;
+  uint32_t x[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) x[k] = p[k];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+    h[k] = big ? __builtin_bswap32(v) : v;
+  }
+}
+
+// Is LDS offset r a plausible record start on its own header (and does its payload fit)?
+__device__ __forceinline__ bool head_ok(const SpecCtx &c, const uint32_t (&h)[4], uint32_t r) {
+  return c.avail - r >= 16 && plaus(c, h[0], h[1], h[2], h[3]) && c.avail - r - 16 >= h[2];
+}
+
+// How plausible is a start at r whose own header passed head_ok?  1 = weak (fewer than two
+// chained headers could be checked inside the staged window); 2 = strong; 0 = a chained header
+// fails.  Wave-uniform.  A heuristic only: k_emit_tiles verifies every guess; a wrong one costs
+// a wait or a re-walk, never a result.
+__device__ __forceinline__ int chain_grade(const SpecCtx &c, const uint32_t *w, uint32_t r, uint32_t ts, uint32_t incl) {
   uint32_t q = r + 16 + incl;
   int ver = 0;
   for (int hop = 0; hop < 3; ++hop) {
@@ -613,6 +756,38 @@ __device__ __forceinline__ int grade(const SpecCtx &c, const uint32_t *w, uint32
     if (c.avail - q - 16 < incl2) return ver >= 2 ? 2 : 1;
     ts = ts2;
     q += 16 + incl2;
+  }
+  return 2;
+}
+
+// chain_grade() in ONE parallel LDS read: lanes 1..3 read the headers of hops 1..3 at the
+// positions they have if the candidate's record length repeats.  Returns chain_grade()'s answer
+// when every hop it needs sits where assumed, else -1 (the caller then hops serially).
+__device__ __forceinline__ int stride_grade(const SpecCtx &c, const uint32_t *w, uint32_t r, uint32_t ts, uint32_t incl) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t k = lane >= 1u && lane <= 3u ? lane : 0u;
+  const uint32_t q = r + k * (16u + incl);
+  const bool in_stage = k != 0u && q + 16u <= (uint32_t)kStage;
+  uint32_t h[4];
+  hdr4(w, in_stage ? q : 0u, c.big, h);
+  const uint32_t myts = lane == 0u ? ts : h[0];
+  const uint32_t prev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)myts, 0x111, 0xf, 0xf, false);  // row_shr:1
+  const uint64_t eof = __ballot(k && q == c.avail && c.exact_end);
+  const uint64_t stage = __ballot(k && !in_stage);
+  const uint64_t shrt = __ballot(k && c.avail - q < 16u);
+  const uint64_t pass = __ballot(k && plaus(c, h[0], h[1], h[2], h[3]) && h[0] - prev + kTsWindow <= 2u * kTsWindow);
+  const uint64_t cut = __ballot(k && c.avail - q - 16u < h[2]);
+  const uint64_t same = __ballot(k && h[2] == incl);
+  int ver = 0;
+  for (int i = 1; i <= 3; ++i) {
+    const uint64_t b = 1ull << i;
+    if (i >= 2 && !(same & (b >> 1))) return -1;  // hop i is not where the stride puts it
+    if (eof & b) return 2;
+    if (stage & b) return ver >= 2 ? 2 : 1;
+    if (shrt & b) return ver >= 1 ? 2 : 1;
+    if (!(pass & b)) return 0;
+    ++ver;
+    if (cut & b) return ver >= 2 ? 2 : 1;
   }
   return 2;
 }
@@ -675,9 +850,14 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
 }
 
 // diagnostics (DIAG kernel variants only: the production kernels carry none of this)
-template <bool DIAG>
-__device__ __forceinline__ void stamp(const ParseParams &kp, uint32_t t, int k) {
-  if (DIAG && kp.stamps && (threadIdx.x & 63u) == 0) kp.stamps[(uint64_t)t * kStampWords + k] = __builtin_amdgcn_s_memrealtime();
+struct Stamps {  // kept in registers, written once at the end (a store per stamp would make
+  uint64_t v[kStampWords];  // later vmcnt waits wait for it and skew what is measured)
+};
+__device__ __forceinline__ void stamp_at(Stamps &st, int k) { st.v[k] = __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void stamp_flush(const ParseParams &kp, const Stamps &st, uint32_t t, uint32_t mask) {
+  if (kp.stamps && (threadIdx.x & 63u) == 0)
+    for (int k = 0; k < kStampWords; ++k)
+      if (mask & (1u << k)) kp.stamps[(uint64_t)t * kStampWords + k] = st.v[k];
 }
 
 // LDS written by some lanes of this wave, then read by others: LDS executes one wave's requests
@@ -690,27 +870,40 @@ __device__ __forceinline__ void wave_sync() {
 typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
 // speculation context of this launch: ts_usec bound from the file magic, the first record's
 // ts_sec as a reference (both read once per wave)
-__device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp) {
+// Issue the (byte) loads of the speculation context: lanes 0..3 the pcap magic, lanes 4..7 the
+// reference record's ts_sec (range-checked: a byte outside the input reads 0).  spec_ctx()
+// finishes it once the loads landed.
+__device__ __forceinline__ uint32_t spec_ctx_load(const ParseParams &kp) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const bool has_ref = kp.ref != kNone && kp.len >= kp.ref + 16;
+  const uint64_t lim = kp.len < 0x7fffffffull ? kp.len : 0x7fffffffull;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)kp.buf, 0, (int)lim, 0x00020000);
+  uint32_t off = lane < 4 ? lane : (uint32_t)(has_ref && kp.ref < 0x7ffffff0ull ? kp.ref : 0x7ffffff0ull) + (lane - 4);
+  if (lane >= 8) off = 0x7ffffff0u;  // out of range: 0
+  return __builtin_amdgcn_raw_buffer_load_b8(rs, (int)off, 0, 0);
+}
+// speculation context of this launch: ts_usec bound from the file magic, the first record's
+// ts_sec as a reference
+__device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp, uint32_t b) {
   SpecCtx sc;
   sc.big = kp.big;
-  sc.frac_max = kp.frac_max;
-  if (kp.flags & kFlagMagicAtZero) {  // microsecond pcap magic: ts_usec < 1e6
-    GlobalReader gm{kp.buf, 4};
-    const uint32_t m = gm.le32(0);
-    if (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u) sc.frac_max = 1000000u;
-  }
+  uint32_t v = b << (8 * (threadIdx.x & 3u));
+  v |= __shfl_xor((int)v, 1, 64);
+  v |= __shfl_xor((int)v, 2, 64);
+  const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)v, 0);
+  const uint32_t r = (uint32_t)__builtin_amdgcn_readlane((int)v, 4);
+  // microsecond pcap magic (either byte order) at byte 0: ts_usec < 1e6
+  sc.frac_max = ((kp.flags & kFlagMagicAtZero) && (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u)) ? 1000000u : kp.frac_max;
   sc.has_ref = kp.ref != kNone && kp.len >= kp.ref + 16;
-  GlobalReader gr{kp.buf + (sc.has_ref ? kp.ref : 0ull), sc.has_ref ? 4ull : 0ull};
-  const uint32_t v = gr.le32(0);
-  sc.ts_ref = __builtin_amdgcn_readfirstlane(kp.big ? __builtin_bswap32(v) : v);
-  sc.frac_max = __builtin_amdgcn_readfirstlane(sc.frac_max);
+  sc.ts_ref = kp.big ? __builtin_bswap32(r) : r;
   sc.avail = 0;
   sc.exact_end = true;
   return sc;
 }
 
-// first strong (else first weak) record-start candidate in [0, span) of the staged tile, 64
-// candidates per round; kNone if neither (wave-uniform)
+// First strong (else first weak) record start in [lo, span) of the staged tile; kNone if
+// neither (wave-uniform).  64 candidates per round are screened on their own header (one
+// 16-B read per lane); only the survivors, in offset order, have their chain graded.
 __device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
                               uint32_t span) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -720,11 +913,20 @@ __device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t 
   uint32_t weak = 0xffffffffu;
   for (uint32_t base = lo; base < span; base += 64) {
     const uint32_t r = base + lane;
-    const int g = r < span ? grade(sc, w, r) : 0;
-    const uint64_t b2 = __ballot(g == 2);
-    if (b2) return tile_lo + base + (uint32_t)__builtin_ctzll(b2);
-    const uint64_t b1 = __ballot(g == 1);
-    if (weak == 0xffffffffu && b1) weak = base + (uint32_t)__builtin_ctzll(b1);
+    uint32_t h[4];
+    hdr4(w, r < span ? r : 0u, sc.big, h);
+    uint64_t m = __ballot(r < span && head_ok(sc, h, r));
+    while (m) {
+      const int j = __builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t c = base + (uint32_t)j;
+      const uint32_t ts = (uint32_t)__builtin_amdgcn_readlane((int)h[0], j);
+      const uint32_t incl = (uint32_t)__builtin_amdgcn_readlane((int)h[2], j);
+      int g = stride_grade(sc, w, c, ts, incl);
+      if (g < 0) g = chain_grade(sc, w, c, ts, incl);  // record lengths differ: hop by hop
+      if (g == 2) return tile_lo + base + (uint32_t)j;
+      if (g == 1 && weak == 0xffffffffu) weak = base + (uint32_t)j;
+    }
   }
   return weak == 0xffffffffu ? kNone : tile_lo + weak;
 }
@@ -741,21 +943,14 @@ __device__ __forceinline__ void put_v6(uint32_t *row, const FlowWords &f) {
   d[1] = u32x4{f.v6[4], f.v6[5], f.v6[6], f.v6[7]};
 }
 
-// ---- LDS-DMA staging ring (per wave) -------------------------------------------------------
-// Tiles land in LDS straight from HBM (`buffer_load_dwordx4 ... lds`, 1 KiB per instruction,
-// range-checked: bytes past the input read 0) with no registers held in flight.  The next
-// tile's DMA is issued before the wait for the current one, so the youngest vector-memory
-// instructions at the wait are exactly the next tiles' DMAs: `s_waitcnt vmcnt(k * per-tile)`
-// retires the current tile and nothing later, whatever stores came before.
-#ifndef NPR_RING
-#define NPR_RING 2
-#endif
-constexpr int kRing = NPR_RING;       // tiles staged per wave (1 processed + kRing-1 in flight)
-constexpr int kRows = kTile / 1024;   // 1-KiB rows of a tile (16-B DMA), then one 256-B halo row (4-B DMA)
-constexpr int kSlotWords = kTile / 4 + 64;
-constexpr int kDmaScan = kRows + 1;   // DMA instructions per tile, pass 1
-constexpr int kDmaEmit = kRows + 4;   // + 2 record-offset rows + 1 aggregate row, pass 2
-static_assert(kTile % 1024 == 0 && kHalo <= 256 - 80, "halo row must hold the halo + the decode over-read");
+
+// ---- LDS-DMA staging --------------------------------------------------------------------------
+// A tile lands in LDS straight from HBM (`buffer_load_dwordx4 ... lds`, 1 KiB per instruction,
+// range-checked: bytes past the input read 0) with no registers held in flight: kTile/1024 rows
+// of 16 B per lane, then one 256-B halo row of 4 B per lane.
+constexpr int kRows = kTile / 1024;
+constexpr int kSlotWords = kTile / 4 + 64;  // tile + 256-B halo row (>= kStage + the decoder's 72-B over-read)
+static_assert(kHalo <= 256 - 80, "halo row must hold the halo + the decode over-read");
 typedef __attribute__((address_space(3))) void *lds_ptr_t;
 
 __device__ __forceinline__ void dma_tile(const ParseParams &kp, uint64_t tile_lo, uint32_t *dst) {
@@ -769,518 +964,311 @@ __device__ __forceinline__ void dma_tile(const ParseParams &kp, uint64_t tile_lo
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + i * 256), 16, (lane + 64u * (uint32_t)i) * 16u, 0, 0, 0);
   __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)(dst + kRows * 256), 4, (uint32_t)kTile + lane * 4u, 0, 0, 0);
 }
-// pass 2 extras: pass 1's record-offset pairs of tile t and its A granules (dwords 0..5), sc1
-__device__ __forceinline__ void dma_extras(const ParseParams &kp, uint32_t t, uint32_t *off, uint32_t *agg) {
+// pass 1's record offsets of tile t (kMaxRec u16) -> LDS
+__device__ __forceinline__ void dma_offsets(const ParseParams &kp, uint32_t t, uint16_t *dst) {
   const uint32_t lane = threadIdx.x & 63u;
-  const __amdgpu_buffer_rsrc_t ro =  // light mode has no offset scratch: an empty range reads nothing
-      __builtin_amdgcn_make_buffer_rsrc(kp.srec_g ? (void *)(kp.srec_g + (uint64_t)t * kMaxRec) : (void *)kp.slots, 0,
-                                        kp.srec_g ? kMaxRec * 2 : 0, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)off, 4, lane * 4u, 0, 0, 16);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)(off + 64), 4, lane * 4u + 256u, 0, 0, 16);
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.slots + t), 0, 24, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (lds_ptr_t)agg, 4, lane * 4u, 0, 0, 16);
+  const __amdgpu_buffer_rsrc_t ro =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, kMaxRec * 2, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < kMaxRec / 128; ++i)
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(ro, (lds_ptr_t)(reinterpret_cast<uint32_t *>(dst) + i * 64), 4,
+                                             lane * 4u + 256u * (uint32_t)i, 0, 0, 0);
 }
-// wait until at most `ahead` tiles' DMAs (of `per` instructions each) are outstanding
-template <int PER>
-__device__ __forceinline__ void wait_dma(uint32_t ahead) {
-  constexpr int w1 = PER, w2 = 2 * PER;
-  static_assert(2 * PER < 64, "vmcnt field is 6 bits");
-  if (ahead == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
-  else if (ahead == 1 || kRing <= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (w1 & 15) | ((w1 >> 4) << 14));
-  else __builtin_amdgcn_s_waitcnt(0x0F70 | (w2 & 15) | ((w2 >> 4) << 14));
-  wave_sync();  // LDS reads of the landed tile stay below the wait
+__device__ __forceinline__ void wait_all_vmem() {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  wave_sync();                         // LDS reads of the landed bytes stay below the wait
 }
 
-struct ParseShared {  // one wave's LDS
-  uint32_t data[kRing][kSlotWords];     // tile + 256-B halo row (>= kStage bytes + the decoder's 72-B over-read)
-  uint32_t off[kRing][kMaxRec / 2];     // pass 2: pass 1's record-offset pairs (DMA)
-  uint32_t agg[kRing][64];              // pass 2: the tile's A granules (DMA, dwords 0..5)
-  uint16_t srec[2 * kMaxRec];           // record offsets (+ room for the walk's unconditional stores)
+struct TileShared {  // one wave's LDS
+  uint32_t data[kSlotWords];   // the staged tile + halo
+  uint16_t srec[2 * kMaxRec];  // record offsets (+ room for the walk's unconditional stores)
 };
 
-__device__ __forceinline__ void publish_fold(const ParseParams &kp, GroupSlot *G, const Seg &c, int64_t first) {
-  const uint32_t ep = kp.epoch;
-  const uint64_t mrel = c.valid ? 0ull : (uint64_t)(c.mism - first) & 0x7fffull;
-  st_agent(&G->g[0], gran(ep, c.exit));
-  st_agent(&G->g[1], gran(ep, c.entry == kNone ? 0ull : c.entry + 1));
-  st_agent(&G->g[2], gran(ep, c.cnt));
-  st_agent(&G->g[3], gran(ep, (c.ok & 0xffffffffull) | ((uint64_t)c.valid << 32) | (mrel << 33)));
-}
-
-// contiguous tile range [c0, c1) of worker w out of W (balanced)
-__device__ __forceinline__ void chunk_of(uint32_t nt, uint32_t w, uint32_t W, uint32_t &c0, uint32_t &c1) {
-  c0 = (uint32_t)((uint64_t)w * nt / W);
-  c1 = (uint32_t)((uint64_t)(w + 1) * nt / W);
-}
-
-__device__ __forceinline__ uint32_t group_size(const ParseParams &kp, uint32_t g) {
-  return kp.ntiles - (g << 6) < 64u ? kp.ntiles - (g << 6) : 64u;
-}
-
-// group g's last arriver: G1(g), and when g is the last group of block h to finish, G2(h)
-__device__ __forceinline__ void fold_groups(const ParseParams &kp, uint32_t g) {
+// ---------------------------------------------------------------------------------------------
+// pass 1: k_count_tiles — ONE WAVE per tile, no waits on other tiles (bar the folds below).
+//   stage the tile | entry: `start` for tile 0, else a speculated record start | walk ->
+//   record offsets (kept in the scratch for pass 2) | status-only decode -> Ok count |
+//   publish A = {entry, exit, n, Ok count}.  The wave that produced the LAST child of a group
+//   (64 tiles), block (64 groups) or super-block (64 blocks) then folds it: the group's
+//   aggregate and each child's exclusive prefix inside it (chain-consistency monoid).
+// ---------------------------------------------------------------------------------------------
+template <bool DIAG>
+__global__ __launch_bounds__(kWave) void k_count_tiles(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) TileShared sh;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  Seg c;
-  if (!fold_range(kp, 0, (int64_t)g << 6, (int)group_size(kp, g), c, t0)) return;
-  uint32_t last2 = 0;
-  const uint32_t h = g >> 6;
-  const uint32_t hsize = kp.ngroups1 - (h << 6) < 64u ? kp.ngroups1 - (h << 6) : 64u;
+  const uint32_t t = blockIdx.x;
+  Stamps st;
+  const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
+  const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
+  if (DIAG) stamp_at(st, 0);
+  dma_tile(kp, tile_lo, sh.data);
+  const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
+  const bool known = t == 0 && !spec0;  // tile 0 of a capture starts at `start`
+  const uint32_t scb = known ? 0u : spec_ctx_load(kp);
+  wait_all_vmem();
+  if (DIAG) stamp_at(st, 1);
+  const uint32_t *w = sh.data;
+
+  uint64_t entry = kp.start;
+  if (!known) {
+    const SpecCtx sc = spec_ctx(kp, scb);
+    const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
+#ifdef NPR_EXP_NOSPEC  // ablation (C2 only): the exact entry of the fixed 80-B stride
+    entry = tile_lo + (uint32_t)((80u - (uint32_t)((tile_lo - 24u) % 80u)) % 80u);
+    (void)sc;
+#else
+    entry = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+#endif
+    if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
+  }
+  entry = uni64(entry);
+  if (DIAG) stamp_at(st, 8);
+  uint32_t n = 0;
+  uint64_t ex = entry == kNone ? 0ull : entry;
+#ifdef NPR_EXP_NOWALK  // ablation (C2 only)
+  n = (uint32_t)((tile_hi - entry + 79) / 80);
+  ex = entry + 80ull * n;
+  sh.srec[lane] = (uint16_t)(entry - tile_lo + 80u * lane);
+#else
+  if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, entry, n);
+#endif
+  ex = uni64(ex);
+  wave_sync();
+  if (DIAG) stamp_at(st, 9);
+
+  // record offsets -> scratch ((n + 1) / 2 u16 pairs; the descriptor's range drops the rest)
+  if (kp.srec_g && n) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(sh.srec);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, (int)(((n + 1) / 2) * 4u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < kMaxRec / 128; ++i)
+      __builtin_amdgcn_raw_buffer_store_b32(src[lane + 64u * (uint32_t)i], rs, (int)(lane * 4u + 256u * (uint32_t)i), 0, 0);
+  }
+  if (DIAG) stamp_at(st, 10);
+  // Ok count: status-only decode of every record
+  uint32_t okc = 0;
+#ifdef NPR_EXP_NOCOUNT  // ablation (C2 only)
+  okc = n;
+  for (int s = 0; s < 0; ++s) {
+#else
+  for (int s = 0; s < kRounds; ++s) {
+#endif
+    if ((uint32_t)s * 64u >= n) break;
+    const uint32_t i = lane + (uint32_t)s * 64u;
+    const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
+    FlowWords f;
+    const bool ok = decode_rec<false>(kp, w, tile_lo, sh.srec[i], f, valid) == NPR_FLOW_OK && valid;
+    okc += (uint32_t)__builtin_popcountll(__ballot(ok));
+  }
+  if (DIAG) stamp_at(st, 11);
   if (lane == 0) {
-    publish_fold(kp, kp.groups1 + g, c, (int64_t)g << 6);
-    __hip_atomic_store(kp.cnt1 + 2 * g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last2 = __hip_atomic_fetch_add(kp.cnt2 + 2 * h, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == hsize - 1u;
+    TileSlot *slot_t = kp.slots + t;
+    const uint32_t ep = kp.epoch;
+    st_agent(&slot_t->a[0], gran(ep, ex));
+    st_agent(&slot_t->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
+    st_agent(&slot_t->a[2], gran(ep, (uint64_t)n | ((uint64_t)okc << 24)));
   }
-  if (__builtin_amdgcn_readfirstlane(last2) && fold_range(kp, 1, (int64_t)h << 6, (int)hsize, c, t0) && lane == 0) {
-    publish_fold(kp, kp.groups2 + h, c, (int64_t)h << 12);
-    __hip_atomic_store(kp.cnt2 + 2 * h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// pass 1: scan_chunk — ONE WAVE owns the contiguous tiles [c0, c1) and never waits on another
-// wave (no workgroup barriers anywhere).  Per tile: (the next tile -> LDS by DMA) | entry = the
-// previous tile's exit while the chain continues, else a speculated start | walk -> record
-// offsets, also kept in the offset scratch for pass 2 | status-only decode -> Ok count (light
-// mode: decode with fields, Ok flows parked) | publish A = {entry, exit, n, Ok count}.  At the
-// end of the chunk the wave arrives once at each 64-tile group it touched: the arrival that
-// completes a group folds its G1, and the group that completes a 4096-tile block folds G2.
-// ---------------------------------------------------------------------------------------------
-template <bool DIAG, bool LIGHT>
-__device__ __forceinline__ void scan_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (int k = 0; k < kRing - 1; ++k)
-    if (c0 + k < c1) dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
-  const SpecCtx sc = spec_ctx(kp);
-  uint64_t carry = kNone;  // exact continuation of the chain
-  uint64_t chunk_ok = 0;   // light mode: Ok flows parked so far in this chunk
-  for (uint32_t t = c0; t < c1; ++t) {
-    const uint32_t slot = (t - c0) % kRing;
-    const uint32_t *w = sh.data[slot];
-    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    stamp<DIAG>(kp, t, 0);
-    // refill the slot processed last iteration with the tile kRing-1 ahead, then wait for this one
-    const uint32_t ahead = c1 - 1 - t < (uint32_t)(kRing - 1) ? c1 - 1 - t : (uint32_t)(kRing - 1);
-    if (t + kRing - 1 < c1) dma_tile(kp, tile_lo + (uint64_t)(kRing - 1) * kTile, sh.data[(slot + kRing - 1) % kRing]);
-    wait_dma<kDmaScan>(ahead);
-
-    uint64_t entry = carry;
-    const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
-    if (t == 0 && !spec0) {
-      entry = kp.start;
-    } else if (carry == kNone) {
-      const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
-      entry = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
-      if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
-    }
-    stamp<DIAG>(kp, t, 1);
-    entry = uni64(entry);
-    uint32_t n = 0;
-    uint64_t ex = entry == kNone ? 0ull : entry;
-    if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, entry, n);
-    ex = uni64(ex);
-    wave_sync();
-    stamp<DIAG>(kp, t, 2);
-
-    // ---- full mode: offsets -> scratch (pairs of u16) + Ok count (status-only decode);
-    //      light mode: decode with fields, Ok flows parked in tile order
-    if (!LIGHT && kp.srec_g) {  // (n + 1) / 2 offset pairs; the descriptor's range drops the rest
-      const uint32_t *src = reinterpret_cast<const uint32_t *>(sh.srec);
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          (void *)(kp.srec_g + (uint64_t)t * kMaxRec), 0, (int)(((n + 1) / 2) * 4u), 0x00020000);
-      __builtin_amdgcn_raw_buffer_store_b32(src[lane], rs, (int)(lane * 4u), 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b32(src[lane + 64], rs, (int)(lane * 4u + 256u), 0, 0);
-    }
-    uint32_t okc = 0;
-    for (int s = 0; s < kRounds; ++s) {
-      if ((uint32_t)s * 64u >= n) break;
-      const uint32_t i = lane + (uint32_t)s * 64u;
-      const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
-      FlowWords f;
-      const uint32_t rel = sh.srec[i];
-      const bool ok = decode_rec<LIGHT>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
-      const uint64_t bal = __ballot(ok);
-      if (LIGHT && ok) {  // parked contiguously per chunk, in chain order (<= kMaxOk per tile)
-        const uint64_t row = ((uint64_t)c0 * kMaxOk + chunk_ok + okc + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull))) * 8;
-        put_flow(kp.park + row, f, tile_lo + rel);
-        if (kp.park_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.park_v6 + row, f);
-      }
-      okc += (uint32_t)__builtin_popcountll(bal);
-    }
-    stamp<DIAG>(kp, t, 3);
-    if (lane == 0) {
-      TileSlot *slot_t = kp.slots + t;
-      const uint32_t ep = kp.epoch;
-      st_agent(&slot_t->a[0], gran(ep, ex));
-      st_agent(&slot_t->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
-      st_agent(&slot_t->a[2], gran(ep, (uint64_t)n | ((uint64_t)okc << 24)));
-    }
-    // the chain continues into the next tile unless it ended here (Q3) or nothing was found
-    carry = uni64((entry != kNone && ex >= tile_hi) ? ex : kNone);
-    chunk_ok += okc;
-    stamp<DIAG>(kp, t, 4);
-    wave_sync();  // done with this slot's LDS before it is refilled
-  }
-  // arrive at the chunk's groups (one add per group; the add that completes a group folds it)
-  stamp<DIAG>(kp, c0, 11);
-  for (uint32_t g = c0 >> 6; g <= (c1 - 1) >> 6; ++g) {
-    const uint32_t lo = c0 > (g << 6) ? c0 : (g << 6), hi = c1 < ((g + 1) << 6) ? c1 : ((g + 1) << 6);
-    uint32_t last = 0;
-    if (lane == 0)
-      last = __hip_atomic_fetch_add(kp.cnt1 + 2 * g, hi - lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + (hi - lo) ==
-             group_size(kp, g);
-    if (__builtin_amdgcn_readfirstlane(last)) fold_groups(kp, g);
-  }
-  stamp<DIAG>(kp, c0, 12);
-}
-
-// ---------------------------------------------------------------------------------------------
-// pass 2: emit_chunk — ONE WAVE owns the contiguous tiles [c0, c1).
-//   exact prefix before c0 = start ⊕ G2(blocks) ⊕ G1(groups) ⊕ A(tiles): the three 64-wide
-//   windows are loaded together, then folded; a contradiction (a mis-speculated tile m < c0)
-//   is settled by m's exact prefix P(m), published below by m's owner.  Then per tile,
-//   carrying the exact chain position and counts: (the next tile, its A granules and pass 1's
-//   record offsets -> LDS by DMA) | the offsets: pass 1's when its entry equals the exact
-//   position (the common case), else a walk | decode every record | record table / status |
-//   Ok flows at their convert_records (reverse-order) positions, ranked by ballot | publish P(t).
-// ---------------------------------------------------------------------------------------------
-// The chain's anchor: `start`, or with kFlagSpecStart the entry pass 1 speculated for tile 0
-// (none found: the range yields nothing and reports NPR_NO_ENTRY; the chain passes `stop`).
-__device__ bool anchor_of(const ParseParams &kp, Seg &X, uint64_t &entry0, uint64_t t0) {
-  X = start_seg(kp);
-  entry0 = kp.start;
-  if (!(kp.flags & kFlagSpecStart)) return true;
-  for (;;) {
-    const uint64_t a1 = uni64(ld_agent(&kp.slots[0].a[1]));
-    if (tagged(a1, kp.epoch)) {
-      const uint64_t e1 = a1 & kMask48;
-      entry0 = e1 ? e1 - 1 : kNone;
-      X.entry = X.exit = e1 ? e1 - 1 : kp.stop;
-      return true;
-    }
-    if (!spin_ok(kp, t0)) return false;
-  }
-}
-
-// exact chain state before tile c: false when a hand-off timed out
-__device__ bool prefix_of(const ParseParams &kp, uint32_t c, Seg &X, uint64_t &entry0) {
-  const uint32_t lane = threadIdx.x & 63u;
+  if (DIAG) stamp_at(st, 2);
+  // Fold the group this tile is the folder of, then (when that group is the last of its block)
+  // the block, then the super-block.  A group's folder is one of its last 8 tiles, rotating with
+  // the group index: consecutive tiles are dealt round-robin over the 8 XCDs, so a fixed member
+  // (say the last) would put every fold wait on one XCD and leave it trailing the others.  The
+  // folder waits (bounded) for its group's tiles, all dispatched at most 7 tiles after it.
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  if (!anchor_of(kp, X, entry0, t0)) return false;
-  const int64_t h = c >> 12, g = c >> 6;
-  if (h > 64) return prefix_generic(kp, X, 0, c, X, t0);  // > 1 GiB before c: the generic walker
-  const int n2 = (int)h, n1 = (int)(g - (h << 6)), n0 = (int)((int64_t)c - (g << 6));
-  // all three windows in flight at once
-  const LaneSeg L2 = load_agg(kp, 2, h - 1 - lane, (int)lane < n2);
-  const LaneSeg L1 = load_agg(kp, 1, g - 1 - lane, (int)lane < n1);
-  const LaneSeg L0 = load_agg(kp, 0, (int64_t)c - 1 - lane, (int)lane < n0);
-  const bool all = __ballot(((int)lane < n2 && !L2.present) || ((int)lane < n1 && !L1.present) ||
-                            ((int)lane < n0 && !L0.present)) == 0ull;
-  Seg y;
-  if (all) {
-    if (n2) X = combine(kp, X, fold_window(kp, L2, n2 - 1));
-    if (n1) X = combine(kp, X, fold_window(kp, L1, n1 - 1));
-    if (n0) X = combine(kp, X, fold_window(kp, L0, n0 - 1));
-  } else {  // not all published yet (fused launch): fold each window as it completes
-    if (n2) {
-      if (!fold_range(kp, 2, 0, n2, y, t0)) return false;
-      X = combine(kp, X, y);
-    }
-    if (n1) {
-      if (!fold_range(kp, 1, h << 6, n1, y, t0)) return false;
-      X = combine(kp, X, y);
-    }
-    if (n0) {
-      if (!fold_range(kp, 0, g << 6, n0, y, t0)) return false;
-      X = combine(kp, X, y);
+  const int64_t grp = t >> 6;
+  const int64_t glast = (grp << 6) + 63 < (int64_t)kp.ntiles - 1 ? (grp << 6) + 63 : (int64_t)kp.ntiles - 1;
+  const int64_t folder = (grp << 6) + 56 + (grp & 7) < glast ? (grp << 6) + 56 + (grp & 7) : glast;
+  if ((int64_t)t == folder) {
+    int64_t idx = grp;
+    for (int lvl = 1; lvl <= kLevels; ++lvl) {
+      if (!fold_children<DIAG>(kp, lvl, idx, t0)) break;
+      const int64_t nself = (int64_t)kp.ngroups[lvl];  // elements of this level
+      const int64_t par = idx >> 6;
+      const int64_t plast = (par << 6) + 63 < nself - 1 ? (par << 6) + 63 : nself - 1;
+      if (idx != plast || lvl == kLevels) break;  // the parent is folded by its last child's folder
+      idx = par;
     }
   }
-  if (!X.valid) return prefix_generic(kp, X, 0, c, X, t0);
-  return true;
-}
-
-__device__ __forceinline__ void emit_prologue(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
-#pragma unroll
-  for (int k = 0; k < kRing - 1; ++k)
-    if (c0 + k < c1) {
-      dma_tile(kp, kp.org + (uint64_t)(c0 + k) * kTile, sh.data[k]);
-      dma_extras(kp, c0 + k, sh.off[k], sh.agg[k]);
-    }
-}
-
-// Tiles [c0, c1) from the exact chain state (pos, pcnt, pok); emit_prologue has been issued.
-template <bool DIAG>
-__device__ void emit_tiles(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1, uint64_t pos,
-                           uint64_t pcnt, uint64_t pok, uint64_t entry0) {
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint32_t t = c0; t < c1; ++t) {
-    const uint32_t slot = (t - c0) % kRing;
-    const uint32_t *w = sh.data[slot];
-    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    stamp<DIAG>(kp, t, 5);
-    const uint32_t ahead = c1 - 1 - t < (uint32_t)(kRing - 1) ? c1 - 1 - t : (uint32_t)(kRing - 1);
-    if (t + kRing - 1 < c1) {
-      const uint32_t ns = (slot + kRing - 1) % kRing;
-      dma_tile(kp, tile_lo + (uint64_t)(kRing - 1) * kTile, sh.data[ns]);
-      dma_extras(kp, t + kRing - 1, sh.off[ns], sh.agg[ns]);
-    }
-    wait_dma<kDmaEmit>(ahead);
-    const uint32_t *ag = sh.agg[slot];
-    const uint64_t a1 = uni64((uint64_t)ag[2] | ((uint64_t)ag[3] << 32));
-    const uint64_t a2 = uni64((uint64_t)ag[4] | ((uint64_t)ag[5] << 32));
-    const bool reuse = kp.srec_g && tagged(a1, kp.epoch) && tagged(a2, kp.epoch) && (a1 & kMask48) == pos + 1;
-    // the record offsets: pass 1's (same exact entry) or a walk from the exact position
-    const uint16_t *srec = reuse ? reinterpret_cast<const uint16_t *>(sh.off[slot]) : sh.srec;
-    uint32_t n = 0;
-    uint64_t ex = pos;
-    if (pos >= tile_lo && pos < tile_hi) {
-      if (reuse) {
-        n = (uint32_t)(a2 & 0xffffffull);
-        if (n) {  // exit = just past the last record (the walk advances by whole records)
-          const uint32_t rl = __builtin_amdgcn_readfirstlane(srec[n - 1]);
-          ex = tile_lo + rl + 16u + __builtin_amdgcn_readfirstlane(hdr(w, rl, 2, kp.big));
-        }
-      } else {
-        ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n);
-        wave_sync();
-        if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
-      }
-    }
-    stamp<DIAG>(kp, t, 6);
-
-    // ---- decode, record table, Ok flows at reverse positions (rank = ballot prefix)
-    uint32_t okbase = 0;
-    for (int s = 0; s < kRounds; ++s) {
-      if ((uint32_t)s * 64u >= n) break;
-      const uint32_t i = lane + (uint32_t)s * 64u;
-      const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
-      FlowWords f;
-      const uint32_t rel = srec[i];
-      const uint32_t st = decode_rec<true>(kp, w, tile_lo, rel, f, valid);
-      const bool ok = st == NPR_FLOW_OK && valid;
-      if (valid && (kp.rec_status || kp.rec_off || kp.recs)) {
-        const uint64_t p = tile_lo + rel;
-        const uint64_t idx = pcnt + i;
-        if (idx < kp.rec_cap) {
-          if (kp.rec_status) kp.rec_status[idx] = (uint8_t)st;
-          if (kp.rec_off) kp.rec_off[idx] = p;
-          if (kp.recs) {
-            const bool big = kp.big;
-            uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
-            row[0] = p;
-            row[1] = (uint64_t)hdr(w, rel, 0, big) | ((uint64_t)hdr(w, rel, 1, big) << 32);
-            row[2] = (uint64_t)hdr(w, rel, 2, big) | ((uint64_t)hdr(w, rel, 3, big) << 32);
-          }
-        }
-      }
-      const uint64_t bal = __ballot(ok);
-      if (ok && kp.flows) {
-        const uint64_t fi = pok + okbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-        if (fi < kp.flow_cap) {
-          const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
-          put_flow(kp.flows + o * 8, f, tile_lo + rel);
-          if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.flows_v6 + o * 8, f);
-        }
-      }
-      okbase += (uint32_t)__builtin_popcountll(bal);
-    }
-    pos = uni64(ex);
-    pcnt += n;
-    pok += okbase;
-    if (lane == 0) {
-      const uint32_t ep = kp.epoch;
-      TileSlot *slot_t = kp.slots + t;
-      st_agent(&slot_t->p[0], gran(ep, pos));
-      st_agent(&slot_t->p[1], gran(ep, pcnt));
-      st_agent(&slot_t->p[2], gran(ep, pok));
-      if (t == kp.ntiles - 1) {
-        uint32_t fl = 0;
-        if ((kp.rec_off || kp.recs || kp.rec_status) && pcnt > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
-        if (kp.flows && pok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
-        kp.summary->n_records = pcnt;
-        kp.summary->n_flows = pok;
-        kp.summary->consumed = pos;
-        kp.summary->flags = fl;
-        kp.summary->entry = entry0;
-        kp.summary->epoch = kp.epoch;
-      }
-    }
-    stamp<DIAG>(kp, t, 7);
-    wave_sync();  // done with this slot's LDS before it is refilled
-  }
-}
-
-template <bool DIAG>
-__device__ __forceinline__ void emit_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
-  stamp<DIAG>(kp, c0, 8);
-  emit_prologue(kp, sh, c0, c1);
-  Seg X;
-  uint64_t entry0;
-  stamp<DIAG>(kp, c0, 9);
-  if (!prefix_of(kp, c0, X, entry0)) return;
-  stamp<DIAG>(kp, c0, 10);
-  emit_tiles<DIAG>(kp, sh, c0, c1, uni64(X.exit), uni64(X.cnt), uni64(X.ok), entry0);
+  if (DIAG) stamp_at(st, 3);
+  if (DIAG) stamp_flush(kp, st, t, 0xF0Fu);
 }
 
 // ---------------------------------------------------------------------------------------------
-// pass 2, light mode (flows only): emit_light_chunk — ONE WAVE owns the tiles [c0, c1).
-//   Pass 1 parked the chunk's Ok flows contiguously in chain order.  When the chunk's first tile
-//   started at the exact chain position (the norm), the whole chunk is exact up to a chain END,
-//   so pass 2 is: the exact prefix, the chunk's counts summed up to that END, and ONE contiguous
-//   reversed copy of the parked rows into convert_records order — no staging, walk or decode.
-//   A chunk that started elsewhere runs the full per-tile path (emit_tiles), which also
-//   publishes the exact prefixes P(t) a waiting fold may need.
+// pass 2: k_emit_tiles — ONE WAVE per tile.  The exact chain state before tile t is
+//   anchor ⊕ G3(super-blocks before) ⊕ E(block) ⊕ E(group) ⊕ E(tile)
+// where E(x) is x's exclusive prefix inside its parent, folded by pass 1: four point loads
+// (plus a window of level-3 aggregates past 1 GiB), issued together with the tile's DMA.  A
+// contradiction (a mis-speculated tile m < t) is settled by m's exact prefix P(m), published
+// below by m's own wave.  Then: the record offsets (pass 1's when its entry was the exact
+// position, else a walk) | decode every record | record table / status | Ok flows straight to
+// their convert_records (reverse-order) rows, ranked by ballot | publish P(t).
 // ---------------------------------------------------------------------------------------------
 template <bool DIAG>
-__device__ __forceinline__ void emit_light_chunk(const ParseParams &kp, ParseShared &sh, uint32_t c0, uint32_t c1) {
-  const uint32_t lane = threadIdx.x & 63u;
-  Seg X;
-  uint64_t entry0;
-  stamp<DIAG>(kp, c0, 8);
-  stamp<DIAG>(kp, c0, 9);
-  if (!prefix_of(kp, c0, X, entry0)) return;
-  stamp<DIAG>(kp, c0, 10);
-  const uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);
-  const uint64_t lo0 = kp.org + (uint64_t)c0 * kTile;
-  bool valid = pos < lo0;  // the chain ended before this chunk: nothing here
-  uint64_t n = 0, k = 0, ex = pos;
-  if (!valid) {
-    bool live = true;  // the chunk's chain has not ended yet
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t b = c0; b < c1 && live; b += 64) {
-      const uint32_t cnt = c1 - b < 64u ? c1 - b : 64u;
-      uint64_t w0 = 0, w1 = 0, w2 = 0;
-      for (;;) {  // the chunk's own aggregates (pass 1 published them before this point)
-        if (lane < cnt) {
-          w0 = ld_agent(&kp.slots[b + lane].a[0]);
-          w1 = ld_agent(&kp.slots[b + lane].a[1]);
-          w2 = ld_agent(&kp.slots[b + lane].a[2]);
-        }
-        const bool ok = lane >= cnt || (tagged(w0, kp.epoch) && tagged(w1, kp.epoch) && tagged(w2, kp.epoch));
-        if (__ballot(!ok) == 0ull) break;
-        if (!spin_ok(kp, t0)) return;
-      }
-      if (b == c0) valid = (rl64(w1, 0) & kMask48) == pos + 1;  // the chunk started at the exact position
-      if (!valid) break;
-      for (uint32_t j = 0; j < cnt; ++j) {  // uniform: sum up to (and including) a chain END
-        const uint64_t e = rl64(w0, (int)j) & kMask48, c = rl64(w2, (int)j) & kMask48;
-        n += c & 0xffffffull;
-        k += (c >> 24) & 0xffffffull;
-        ex = e;
-        if (e < tile_end(kp, (int64_t)(b + j))) {  // END (Q3): the rest of the capture is void
-          live = false;
-          break;
-        }
-      }
-    }
-  }
-  if (!valid) {  // mis-speculated run: decode it here from the exact position
-    if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
-    emit_prologue(kp, sh, c0, c1);
-    emit_tiles<DIAG>(kp, sh, c0, c1, pos, pcnt, pok, entry0);
-    return;
-  }
-  stamp<DIAG>(kp, c0, 11);
-  // ONE contiguous copy: parked row j -> flow row flow_cap-1-(pok+j) (convert_records order).
-  // Range-checked buffer accesses (rows past flow_cap are out of range: nothing written).  A plain
-  // two-loads-in-flight loop: the parked rows were just written by pass 1 and are still in L2 /
-  // MALL; deeper batching (4 rows per lane) measured 3x slower here (r21 A/B) — it thrashes them.
-  if (kp.flows && k) {
-    const uint64_t base = (uint64_t)c0 * kMaxOk;
-    const uint64_t kk = pok >= kp.flow_cap ? 0 : (k < kp.flow_cap - pok ? k : kp.flow_cap - pok);  // rows that fit
-    const __amdgpu_buffer_rsrc_t src = __builtin_amdgcn_make_buffer_rsrc((void *)(kp.park + base * 8), 0, (int)(kk * 32), 0x00020000);
-    // destination rows [flow_cap-pok-kk, flow_cap-pok): row j lands at (kk-1-j) in this window
-    const __amdgpu_buffer_rsrc_t dst = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(kp.flows + (kp.flow_cap - pok - kk) * 8), 0, (int)(kk * 32), 0x00020000);
-    for (uint64_t j = lane; j < kk; j += 64) {
-      const u32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(j * 32u), 0, 2);  // nt: read once
-      const u32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(src, (int)(j * 32u + 16u), 0, 2);
-      const uint32_t o = (uint32_t)(kk - 1 - j) * 32u;
-      __builtin_amdgcn_raw_buffer_store_b128(x0, dst, (int)o, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(x1, dst, (int)(o + 16u), 0, 0);
-      if (kp.flows_v6 && (x1[2] >> 16) & NPR_FLOW_KIND_IPV6) {  // IPv6 rows: their parked side row too
-        const u32x4 *s6 = reinterpret_cast<const u32x4 *>(kp.park_v6 + (base + j) * 8);
-        u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + (kp.flow_cap - 1 - (pok + j)) * 8);
-        d6[0] = s6[0], d6[1] = s6[1];
-      }
-    }
-  }
-  stamp<DIAG>(kp, c0, 12);
-  if (c1 == kp.ntiles && lane == 0) {  // this run holds the capture's last tile
-    const uint64_t tot_rec = pcnt + n, tot_ok = pok + k;
-    uint32_t fl = 0;
-    if (kp.flows && tot_ok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
-    kp.summary->n_records = tot_rec;
-    kp.summary->n_flows = tot_ok;
-    kp.summary->consumed = ex;
-    kp.summary->flags = fl;
-    kp.summary->entry = entry0;
-    kp.summary->epoch = kp.epoch;
-  }
-}
-
-// pass 1 alone / pass 2 alone (two launches; diagnostics) and both fused in one persistent grid:
-// a wave moves from its scan chunk straight to its emit chunk, whose prefix fold waits only for
-// the aggregates of earlier chunks (lower, earlier-dispatched workgroups: no deadlock).
-template <bool DIAG, bool LIGHT>
-__global__ __launch_bounds__(kWave) void k_scan_tiles(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ParseShared sh;
-  uint32_t c0, c1;
-  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
-  if (c0 < c1) scan_chunk<DIAG, LIGHT>(kp, sh, c0, c1);
-}
-template <bool DIAG, bool LIGHT>
 __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ParseShared sh;
-  uint32_t c0, c1;
-  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
-  if (c0 >= c1) return;
-  if (LIGHT) emit_light_chunk<DIAG>(kp, sh, c0, c1);
-  else emit_chunk<DIAG>(kp, sh, c0, c1);
-}
-template <bool DIAG, bool LIGHT>
-__global__ __launch_bounds__(kWave) void k_parse_fused(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ParseShared sh;
-  uint32_t c0, c1;
-  chunk_of(kp.ntiles, blockIdx.x, gridDim.x, c0, c1);
-  if (c0 >= c1) return;
-  scan_chunk<DIAG, LIGHT>(kp, sh, c0, c1);
-  if (LIGHT) emit_light_chunk<DIAG>(kp, sh, c0, c1);
-  else emit_chunk<DIAG>(kp, sh, c0, c1);
-}
+  __shared__ __attribute__((aligned(16))) TileShared sh;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t t = blockIdx.x;
+  Stamps st;
+  const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
+  const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
+  if (DIAG) stamp_at(st, 5);
+  dma_tile(kp, tile_lo, sh.data);
+  if (kp.srec_g) dma_offsets(kp, t, sh.srec);
+  // context words, one per lane, from the slot allocation (tile slots, then the level-1/2/3
+  // group slots): A(t) [0,3), E(t) [3,8) (a and e are adjacent), E(group) [8,13), E(block)
+  // [13,18), A(0).entry [18] (the anchor of a speculative start)
+  const uint32_t g = t >> 6, h = t >> 12, sup = t >> 18;
+  const uint32_t og1 = (uint32_t)((const char *)kp.groups[1] - (const char *)kp.slots);
+  const uint32_t og2 = (uint32_t)((const char *)kp.groups[2] - (const char *)kp.slots);
+  const uint32_t off = lane < 8u    ? t * 128u + lane * 8u
+                       : lane < 13u ? og1 + g * 128u + 40u + (lane - 8u) * 8u
+                       : lane < 18u ? og2 + h * 128u + 40u + (lane - 13u) * 8u
+                       : lane == 18u ? 8u : 0x7ffffff8u;  // past the range: 0
+  const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void *)kp.slots, 0, 0x7ffffff8, 0x00020000);
+  const uint32_t vlo = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)off, 0, 0);
+  const uint32_t vhi = __builtin_amdgcn_raw_buffer_load_b32(rc, (int)off + 4, 0, 0);
+  wait_all_vmem();
+  const uint64_t v = ((uint64_t)vhi << 32) | vlo;
+  const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
+  if (__ballot(lane < 18u + (spec0 ? 1u : 0u) && !tagged(v, kp.epoch))) return;  // pass 1 aborted
+  if (DIAG) stamp_at(st, 12);
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 
-static int per_cu(const void *k) {
-  int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kWave, 0) != hipSuccess) return 1;
-  return n > 0 ? n : 1;
-}
-// resident one-wave workgroups per CU of the production variants (light = the bench / FFI mode)
-int scan_blocks_per_cu() { return per_cu((const void *)k_scan_tiles<false, true>); }
-int emit_blocks_per_cu() { return per_cu((const void *)k_emit_tiles<false, true>); }
-int fused_blocks_per_cu() { return per_cu((const void *)k_parse_fused<false, true>); }
-
-template <bool DIAG, bool LIGHT>
-static hipError_t launch(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
-  const uint32_t g1 = grid_scan < p.ntiles ? grid_scan : p.ntiles;
-  if (grid_emit == 0) {  // fused
-    hipLaunchKernelGGL((k_parse_fused<DIAG, LIGHT>), dim3(g1), dim3(kWave), 0, s, p);
-    return hipGetLastError();
+  // ---- exact prefix before t: anchor, then E(block), E(group), E(tile).  Fast path: each prefix
+  // is empty, or valid with its entry exactly where the chain stands (then it is a plain sum).
+  uint64_t entry0 = kp.start, xe = kp.start, xc = 0, xo = 0;
+  if (spec0) {
+    const uint64_t e1 = rl64(v, 18) & kMask48;
+    entry0 = e1 ? e1 - 1 : kNone;
+    xe = e1 ? e1 - 1 : kp.stop;
   }
-  const uint32_t g2 = grid_emit < p.ntiles ? grid_emit : p.ntiles;
-  hipLaunchKernelGGL((k_scan_tiles<DIAG, LIGHT>), dim3(g1), dim3(kWave), 0, s, p);
+  bool fast = sup == 0;
+#pragma unroll
+  for (int k = 2; k >= 0; --k) {
+    const int b = k == 2 ? 13 : (k == 1 ? 8 : 3);
+    const uint64_t pok = rl64(v, b + kPreOk);
+    const bool empty = (pok >> 33) & 1ull, valid = (pok >> 32) & 1ull;
+    if (!empty) {
+      const uint64_t en = rl64(v, b + kPreEntry) & kMask48;
+      fast = fast && valid && en == xe + 1;
+      xe = rl64(v, b + kPreExit) & kMask48;
+      xc += rl64(v, b + kPreCnt) & kMask48;
+      xo += pok & 0xffffffffull;
+    }
+  }
+  Seg X;
+  if (fast) {
+    X.exit = xe;
+    X.cnt = xc;
+    X.ok = xo;
+  } else {  // the general monoid: ends, pass-throughs, mis-speculations, > 1 GiB before t
+    X = start_seg(kp);
+    if (spec0) X.entry = X.exit = entry0 == kNone ? kp.stop : entry0;
+    for (int64_t b = 0; b < sup; b += 64) {  // level-3 aggregates before this super-block
+      Seg Y;
+      const int64_t cnt = sup - b < 64 ? sup - b : 64;
+      if (!fold_range(kp, kLevels, b, (int)cnt, Y, t0)) return;
+      X = combine(kp, X, Y);
+    }
+    bool empty;
+    Seg E = prefix_seg(rl64(v, 13), rl64(v, 14), rl64(v, 15), rl64(v, 16), rl64(v, 17), 2, h, empty);
+    if (!empty) X = combine(kp, X, E);
+    E = prefix_seg(rl64(v, 8), rl64(v, 9), rl64(v, 10), rl64(v, 11), rl64(v, 12), 1, g, empty);
+    if (!empty) X = combine(kp, X, E);
+    E = prefix_seg(rl64(v, 3), rl64(v, 4), rl64(v, 5), rl64(v, 6), rl64(v, 7), 0, t, empty);
+    if (!empty) X = combine(kp, X, E);
+    if (!X.valid && !prefix_generic<DIAG>(kp, X, t, t, X, t0)) return;
+  }
+  if (DIAG) stamp_at(st, 6);
+
+  // ---- this tile's records, from the exact chain position
+  const uint64_t pos = uni64(X.exit), pcnt = uni64(X.cnt), pok = uni64(X.ok);
+  const uint64_t a0 = rl64(v, 0) & kMask48, a1 = rl64(v, 1) & kMask48, a2 = rl64(v, 2) & kMask48;
+  uint32_t n = 0;
+  uint64_t ex = pos;
+  if (pos >= tile_lo && pos < tile_hi) {
+    if (kp.srec_g && a1 == pos + 1) {  // pass 1 walked from the exact entry: reuse its offsets
+      n = (uint32_t)(a2 & 0xffffffull);
+      ex = a0;
+    } else {
+      ex = uni64(walk_tile(kp, sh.data, sh.srec, tile_lo, tile_hi, pos, n));
+      wave_sync();
+      if (DIAG && kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, 1u);
+    }
+  }
+  if (DIAG) stamp_at(st, 13);
+  const uint32_t *w = sh.data;
+  uint32_t okbase = 0;
+  for (int s = 0; s < kRounds; ++s) {
+    if ((uint32_t)s * 64u >= n) break;
+    const uint32_t i = lane + (uint32_t)s * 64u;
+    const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
+    FlowWords f;
+    const uint32_t rel = sh.srec[i];
+    const uint32_t st = decode_rec<true>(kp, w, tile_lo, rel, f, valid);
+    const bool ok = st == NPR_FLOW_OK && valid;
+    if (valid && (kp.rec_status || kp.rec_off || kp.recs)) {
+      const uint64_t p = tile_lo + rel;
+      const uint64_t idx = pcnt + i;
+      if (idx < kp.rec_cap) {
+        if (kp.rec_status) kp.rec_status[idx] = (uint8_t)st;
+        if (kp.rec_off) kp.rec_off[idx] = p;
+        if (kp.recs) {
+          const bool big = kp.big;
+          uint64_t *row = reinterpret_cast<uint64_t *>(kp.recs + idx);
+          row[0] = p;
+          row[1] = (uint64_t)hdr(w, rel, 0, big) | ((uint64_t)hdr(w, rel, 1, big) << 32);
+          row[2] = (uint64_t)hdr(w, rel, 2, big) | ((uint64_t)hdr(w, rel, 3, big) << 32);
+        }
+      }
+    }
+    const uint64_t bal = __ballot(ok);
+    if (ok && kp.flows) {
+      const uint64_t fi = pok + okbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+      if (fi < kp.flow_cap) {
+        const uint64_t o = kp.flow_cap - 1 - fi;  // convert_records pops from the end
+        put_flow(kp.flows + o * 8, f, tile_lo + rel);
+        if (kp.flows_v6 && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16))) put_v6(kp.flows_v6 + o * 8, f);
+      }
+    }
+    okbase += (uint32_t)__builtin_popcountll(bal);
+  }
+  if (DIAG) stamp_at(st, 14);
+  const uint64_t ncnt = pcnt + n, nok = pok + okbase;
+  if (lane == 0) {
+    const uint32_t ep = kp.epoch;
+    TileSlot *slot_t = kp.slots + t;
+    st_agent(&slot_t->p[0], gran(ep, ex));
+    st_agent(&slot_t->p[1], gran(ep, ncnt));
+    st_agent(&slot_t->p[2], gran(ep, nok));
+    if (t == kp.ntiles - 1) {
+      uint32_t fl = 0;
+      if ((kp.rec_off || kp.recs || kp.rec_status) && ncnt > kp.rec_cap) fl |= NPR_SUMMARY_RECORD_OVERFLOW;
+      if (kp.flows && nok > kp.flow_cap) fl |= NPR_SUMMARY_FLOW_OVERFLOW;
+      kp.summary->n_records = ncnt;
+      kp.summary->n_flows = nok;
+      kp.summary->consumed = ex;
+      kp.summary->flags = fl;
+      kp.summary->entry = entry0;
+      kp.summary->epoch = kp.epoch;
+    }
+  }
+  if (DIAG) stamp_at(st, 7);
+  if (DIAG) stamp_flush(kp, st, t, 0x70E0u);
+}
+
+template <bool DIAG>
+static hipError_t launch(const ParseParams &p, hipStream_t s) {
+  hipLaunchKernelGGL((k_count_tiles<DIAG>), dim3(p.ntiles), dim3(kWave), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((k_emit_tiles<DIAG, LIGHT>), dim3(g2), dim3(kWave), 0, s, p);
+  hipLaunchKernelGGL((k_emit_tiles<DIAG>), dim3(p.ntiles), dim3(kWave), 0, s, p);
   return hipGetLastError();
 }
 
-hipError_t launch_parse_extract(const ParseParams &p, uint32_t grid_scan, uint32_t grid_emit, hipStream_t s) {
-  const bool diag = p.stats || p.stamps, light = (p.flags & kFlagLight) != 0;
-  if (diag) return light ? launch<true, true>(p, grid_scan, grid_emit, s) : launch<true, false>(p, grid_scan, grid_emit, s);
-  return light ? launch<false, true>(p, grid_scan, grid_emit, s) : launch<false, false>(p, grid_scan, grid_emit, s);
+hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
+  return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -1,17 +1,13 @@
 #!/bin/bash
-# Interleaved A/B of library builds (lib/<name>.so, selected with NPR_LIB) on ONE box, so box-to-box
-# variance cancels.  Usage: ab.sh TAG REPS lib... ; env LIGHT=0|1 (default 1), FUSED=0|1 (default 0).
+# A/B of in-tree library variants (lib/libnpr_*.so via NPR_LIB): bench + stamps each.
+# Usage: bash scripts/ab.sh TAG lib1 lib2 ...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out
-TAG="$1"; REPS="$2"; shift 2
-OUT="$R/gpurun_out/ab_${TAG}.txt"; : > "$OUT"
-for i in $(seq "$REPS"); do
-  for L in "$@"; do
-    NPR_LIB="$R/net-parser-rs_amd/lib/$L" NPR_LIGHT="${LIGHT:-1}" NPR_FUSED="${FUSED:-0}" \
-      timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu > "$R/gpurun_out/ab_${TAG}_cur.log" 2>&1
-    rc=$?; [ $rc -ne 0 ] && { echo "$L rc=$rc" >> "$OUT"; cat "$R/gpurun_out/ab_${TAG}_cur.log" >> "$OUT"; exit $rc; }
-    python -c "import json,sys;d=[json.loads(l) for l in open(sys.argv[1]) if l.startswith('{')][-1];print(sys.argv[2],d['ms_per_step']*1000)" \
-      "$R/gpurun_out/ab_${TAG}_cur.log" "$L" >> "$OUT"
-  done
+TAG=$1; shift
+for L in "$@"; do
+  b=$(basename "$L" .so)
+  NPR_LIB="$R/$L" timeout -k 10 120 python bench.py --steps 100 --warmup 10 --no-cpu > "gpurun_out/ab_${TAG}_$b.json" 2>&1 || exit $?
+  NPR_LIB="$R/$L" timeout -k 10 120 python bench.py --steps 10 --warmup 3 --no-cpu --stats > "gpurun_out/ab_${TAG}_${b}_stats.log" 2>&1 || exit $?
+  cp gpurun_out/stamps_rank0.npy "gpurun_out/stamps_${TAG}_$b.npy"
 done
 exit 0

@@ -14,7 +14,7 @@ run() {  # run <limit-seconds> <log> <cmd...>
   echo "[$(date +%T)] $* -> rc=$rc" | tee -a "$R/gpurun_out/steps.log"
   return $rc
 }
-run 900 "gpu_tests_$TAG.log" python -m pytest tests -m gpu -q -x -p no:cacheprovider
+run 900 "gpu_tests_$TAG.log" python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread
 rc=$?
 if [ $rc -ne 0 ]; then echo "tests failed (rc=$rc): stop"; exit $rc; fi
 run 600 "bench_$TAG.json" python bench.py --steps 50 --warmup 10 || exit $?

@@ -1,35 +1,21 @@
-"""Summarise per-tile phase stamps written by `bench.py --stats` (gpurun_out/stamps_rank0.npy)."""
+"""Per-tile phase timings from bench.py --stats stamps (s_memrealtime, 100 MHz ticks).
+count: [0] start [1] landed [8] entry [9] walked [10] offsets stored [11] counted [2] published [3] folded
+emit:  [5] start [12] context+tile landed [6] prefix known [13] offsets ready [14] decoded+written [7] published"""
 import sys
 
 import numpy as np
 
-s = np.load(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/stamps_rank0.npy").astype(np.int64)
-# two-pass layout: [0] scan tile start [1] entry known [2] walked [3] counted [4] published (+group folds)
-#                  [5] emit tile start [6] walked [7] written
+s = np.load(sys.argv[1]).astype(np.int64)
 t0 = s[:, 0].min()
-us = (s - t0) / 100.0  # s_memrealtime = 100 MHz
-print("tiles", len(s), "scan span us %.2f" % (us[:, 4].max() - us[:, 0].min()),
-      "emit span us %.2f" % (us[:, 7].max() - us[:, 5].min()), "gap us %.2f" % (us[:, 5].min() - us[:, 4].max()))
-for a, b, nm in ((0, 1, "entry"), (1, 2, "walk"), (2, 3, "count"), (3, 4, "pub+fold"), (5, 6, "walk"),
-                 (6, 7, "decode+write"), (0, 4, "scan tile"), (5, 7, "emit tile")):
-    d = us[:, b] - us[:, a]
-    print(f"{nm:14s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
-c0 = s[:, 8] != 0  # chunk-first tiles (stamps 8..12)
-light = c0.any() and not s[:, 5].any()  # light mode: no per-tile emit stamps
-if light:  # chunk stamps [8]=[9] emit start [10] prefix known [11] counts summed [12] copied
-    u = lambda k: (s[c0, k] - t0) / 100.0
-    print("light emit span us %.2f  gap us %.2f" % (u(12).max() - u(8).min(), u(8).min() - us[:, 4].max()))
-    for a, b, nm in ((9, 10, "emit prefix"), (10, 11, "sum counts"), (11, 12, "copy"), (8, 12, "emit chunk")):
-        d = u(b) - u(a)
-        print(f"{nm:16s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
-    print("emit chunk entry pct", np.percentile(u(8), [0, 10, 50, 90, 100]).round(2))
-elif c0.any():
-    u = lambda k: (s[c0, k] - t0) / 100.0
-    for a, b, nm in ((8, 9, "emit prologue"), (9, 10, "emit prefix"), (11, 12, "scan arrive+fold")):
-        d = u(b) - u(a)
-        print(f"{nm:16s} mean {d.mean():6.2f} med {np.median(d):6.2f} p90 {np.percentile(d, 90):6.2f} max {d.max():6.2f}")
-    print("emit chunk entry pct", np.percentile(u(8), [0, 10, 50, 90, 100]).round(2))
-for c, nm in ((0, "scan"), (5, "emit")):
-    e = c + 2 if c == 5 else 4
-    ts = np.linspace(us[:, c].min(), us[:, e].max(), 12)
-    print(nm, "active", [int(((us[:, c] <= x) & (us[:, e] > x)).sum()) for x in ts])
+S = lambda k: (s[:, k] - t0) / 100.0
+med = lambda x: float(np.median(x))
+def chain(name, ks, labels):
+    parts = [f"{labels[i]} {med(S(ks[i+1]) - S(ks[i])):.2f}" for i in range(len(ks) - 1)]
+    print(f"{name}: " + " | ".join(parts))
+chain("count (median us)", [0, 1, 8, 9, 10, 11, 2, 3], ["load", "spec", "walk", "offs", "count", "publish", "fold"])
+chain("emit  (median us)", [5, 12, 6, 13, 14, 7], ["load", "prefix", "offs", "decode+write", "publish"])
+c0, c3, e5, e7 = S(0), S(3), S(5), S(7)
+print(f"count span {c3.max():.2f} us, last start {c0.max():.2f}; emit span {e7.max() - e5.min():.2f} us")
+for name, a, b in (("count", c0, c3), ("emit", e5, e7)):
+    ts = np.linspace(a.min(), b.max(), 16)
+    print(f"{name} live:", [int(((a <= x) & (b > x)).sum()) for x in ts])
