@@ -189,11 +189,15 @@ npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
  * chunk: [8] pass-2 entry [9] prologue issued [10] prefix known [11]/[12] pass-1 group arrival
  * start/end.  out may be NULL with cap 0 to query *n_tiles only. */
 npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_tiles);
-/* Context options.  NPR_OPT_PARK_FLOWS (default 1; env NPR_LIGHT=0 sets 0 at create): a
- * flows-only device parse (no record table / offsets / status requested) parks each tile's Ok
- * flows in pass 1 and pass 2 only reverses them into convert_records order; 0 decodes them in
- * pass 2 instead (the path a launch with a record table always takes).  Same results either way. */
-enum { NPR_OPT_PARK_FLOWS = 1 };
+/* Context options.
+ * NPR_OPT_RESIDENT (default 1; env NPR_RESIDENT=0 sets 0 at create): a flows-only device parse
+ *   (no record table / offsets / status requested) runs the resident single pass: one launch that
+ *   reads the capture once and keeps each wave's decoded flows in registers until the exact
+ *   convert_records rows are known.  0 (and every launch that asks for a record table, offsets or
+ *   status) runs the two-pass kernels; N > 1 caps the resident pass at N waves (longer ranges per
+ *   wave: a test knob).  Same results either way.
+ * NPR_OPT_PARK_FLOWS: accepted for ABI 2 callers, no effect. */
+enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

@@ -35,6 +35,9 @@ struct npr_ctx {
   DevBuf stamps;
   uint64_t stamp_tiles = 0;
   DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
+  int resident = 1;        // NPR_OPT_RESIDENT
+  uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
+  uint64_t res_launches = 0;  // resident launches so far (selects the arrival-counter bank)
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -42,6 +45,8 @@ struct npr_ctx {
 
 namespace {
 
+// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each)
+constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlBytes = kCtlCounters + 2 * kCtlBank;
 constexpr uint32_t kTimeoutTicks = 100u * 1000u * 1000u;  // 1 s of s_memrealtime (100 MHz)
 
 npr_status fail(npr_ctx *c, npr_status st, const char *fmt, ...) {
@@ -138,12 +143,14 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   npr_ctx *c = new npr_ctx();
   c->device = device;
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void **)&c->abort_word, 64) != hipSuccess || hipMalloc((void **)&c->summary, sizeof(npr_summary)) != hipSuccess ||
+      hipMalloc((void **)&c->abort_word, kCtlBytes) != hipSuccess || hipMalloc((void **)&c->summary, sizeof(npr_summary)) != hipSuccess ||
       hipHostMalloc((void **)&c->summary_h, sizeof(npr_summary), 0) != hipSuccess ||
-      hipMemset(c->abort_word, 0, 64) != hipSuccess) {
+      hipMemset(c->abort_word, 0, kCtlBytes) != hipSuccess) {
     npr_ctx_destroy(c);
     return NPR_ERR_DEVICE;
   }
+  const char *env = getenv("NPR_RESIDENT");
+  if (env && env[0] == '0') c->resident = 0;
   *out = c;
   return NPR_OK;
 }
@@ -170,6 +177,10 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
   switch (option) {
     case NPR_OPT_PARK_FLOWS:  // accepted for ABI 2 callers; one decode path since ABI 3
       (void)value;
+      return NPR_OK;
+    case NPR_OPT_RESIDENT:  // 0 off, 1 auto, N > 1: at most N waves (tests: long ranges, deferral)
+      if (value < 0) return fail(c, NPR_ERR_ARG, "NPR_OPT_RESIDENT must be >= 0");
+      c->resident = value;
       return NPR_OK;
     default:
       return fail(c, NPR_ERR_ARG, "unknown option");
@@ -274,7 +285,7 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
     c->epoch = 1;
     HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
-    HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, 64, s));
+    HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, kCtlBytes, s));
   }
   npr::ParseParams p{};
   p.buf = (const uint8_t *)input;
@@ -318,6 +329,24 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
     if ((st = ensure(c, c->stamps, nt * npr::kStampWords * 8, true))) return st;
     p.stamps = (uint64_t *)c->stamps.p;
     c->stamp_tiles = nt;
+  }
+  // flows-only launches: the resident single pass, one wave per (CU x resident waves), at most
+  // kResMaxWaves and at most one per tile
+  if (c->resident && !p.rec_off && !p.recs && !p.rec_status) {
+    if (!c->res_waves) {
+      int cus = 0;
+      HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+      const int per = npr::resident_waves_per_cu();
+      c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
+    }
+    uint64_t wv = std::min<uint64_t>(nt, c->res_waves);
+    if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
+    p.nwaves = (uint32_t)wv;
+    p.rslots = (npr::RangeSlot *)c->slots.p;
+    p.rgroups = p.groups[1];
+    const uint64_t bank = c->res_launches++ & 1u;  // this launch counts in a bank the previous one zeroed
+    p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters + bank * kCtlBank);
+    p.rcnt_next = (uint32_t *)((char *)c->abort_word + kCtlCounters + (bank ^ 1u) * kCtlBank);
   }
   HIP_CHECK(c, npr::launch_parse_extract(p, s));
   return NPR_OK;

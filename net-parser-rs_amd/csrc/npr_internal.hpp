@@ -41,6 +41,20 @@ struct alignas(128) GroupSlot {
   uint64_t e[5];  // prefix words, see kPre*
   uint64_t pad[6];
 };
+// Resident single-pass kernel (k_parse_resident): one slot per wave (its contiguous tile range).
+// a = the range's speculative aggregate {exit, entry + 1, cnt, ok} (phase A); p = the exact
+// inclusive prefix through the range {exit, cnt, ok} (phase B).  The last wave to arrive at a
+// 64-wave group folds it: each member's exclusive prefix (e) and the group aggregate (GroupSlot
+// g); the last group fold folds the groups: each group's exclusive prefix (GroupSlot e).
+struct alignas(128) RangeSlot {
+  uint64_t a[4];
+  uint64_t p[3];
+  uint64_t e[5];  // exclusive prefix inside its 64-wave group (kPre* words), by the group's fold
+  uint64_t pad[4];
+};
+static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
+constexpr uint32_t kResMaxWaves = 64 * 64;  // two fold levels: 64 groups of 64 waves
+
 // exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
 enum : int { kPreExit = 0, kPreCnt = 1, kPreOk = 2, kPreMism = 3, kPreEntry = 4 };
 constexpr int kLevels = 3;  // group levels above the tiles
@@ -88,10 +102,19 @@ struct ParseParams {
   npr_summary *summary;
   uint32_t *stats;         // kStatCount counters or NULL
   uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][kStampWords] or NULL
+  // resident single pass (flows-only launches): 0 = use the two-pass kernels
+  uint32_t nwaves;         // persistent waves, each owning a contiguous tile range (<= kResMaxWaves, <= ntiles)
+  RangeSlot *rslots;       // [nwaves]
+  GroupSlot *rgroups;      // [ceil(nwaves / 64)]
+  uint32_t *rcnt;          // arrival counters (zero at launch): group g at [16 g], the group folds at [16 * 64]
+  uint32_t *rcnt_next;     // the other bank: zeroed by this launch for the next resident launch
 };
 
-// k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each.
+// k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)
+// k_parse_resident, one launch of p.nwaves one-wave workgroups.
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
+// resident waves per CU the hardware admits for k_parse_resident (occupancy query)
+int resident_waves_per_cu();
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);

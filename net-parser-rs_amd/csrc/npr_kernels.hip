@@ -105,6 +105,7 @@ struct GlobalReader {
 struct FlowWords {
   uint32_t d[7];
   uint32_t v6[8];
+  uint32_t v6off;  // payload offset of the IPv6 address block (the resident kernel re-reads it)
 };
 
 // InternetProtocolId::new (src/layer3/mod.rs:54-72)
@@ -208,6 +209,7 @@ __device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f)
     if (FIELDS) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) f.v6[k] = r.le32(sa + 4u * (uint32_t)k);
+      f.v6off = sa;
       f.d[0] = 0;
       f.d[1] = 0;
     }
@@ -317,6 +319,7 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
     f.d[6] = (a[1] & 0xffffu) | ((((v6 ? NPR_FLOW_KIND_IPV6 : 0u) | (proto == 17u ? NPR_FLOW_KIND_UDP : 0u))) << 16);
 #pragma unroll
     for (int k = 0; k < 8; ++k) f.v6[k] = __builtin_amdgcn_alignbyte(a[6 + k], a[5 + k], 2);  // bytes 22..53
+    f.v6off = 22u;
   }
   return (v4 | v6) ? (st3 ? st3 : st4) : 0xffu;
 }
@@ -1258,6 +1261,580 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
   if (DIAG) stamp_flush(kp, st, t, 0x70E0u);
 }
 
+// =============================================================================================
+// RESIDENT SINGLE PASS — k_parse_resident (flows-only launches: the `extract` bench's output)
+//
+// ONE launch of W persistent one-wave workgroups; wave v owns the contiguous tile range
+// [c0(v), c1(v)).  Every byte of the capture is read once:
+//   phase A: the range streams through a per-wave LDS ring (LDS-DMA); the chain is speculated
+//     ONCE, at the range's first tile (wave 0: `start`), then walked tile to tile; every record
+//     is decoded with its fields and the Ok flows of each 64-record round are KEPT IN REGISTERS
+//     (kResSlots rounds; later rounds are deferred to phase B).  The wave publishes its range
+//     aggregate A(v) = {exit, entry, records, Ok flows}; the last wave of each 64-wave group
+//     folds the group's aggregates into G1 (chain-consistency monoid, as for tiles).
+//   phase B: the exact chain state before v = anchor ⊕ G1(groups before) ⊕ A(waves before, in
+//     this group): two 64-wide windows, all produced by LOWER-indexed waves (dispatched
+//     earlier: resident or done, so no co-residency is assumed).  When v's speculated entry is
+//     the exact position (the common case), the register-held flows go straight to their
+//     convert_records rows and only deferred tiles are re-read; otherwise the range is re-walked
+//     from the exact position.  A contradiction below v waits for the offending wave's exact
+//     prefix P(m), published at the end of its own phase B.
+// =============================================================================================
+#ifndef NPR_RES_SLOTS
+#define NPR_RES_SLOTS 6
+#endif
+#ifndef NPR_RES_RING
+#define NPR_RES_RING 2
+#endif
+constexpr int kResSlots = NPR_RES_SLOTS;  // 64-record rounds of flows held in registers per wave
+constexpr int kResRing = NPR_RES_RING;    // LDS tile slots per wave (1 processed + kResRing-1 in flight)
+constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
+static_assert(kResRing >= 2 && (kResRing - 1) * kDmaPer < 64, "vmcnt field is 6 bits");
+
+struct ResShared {  // one wave's LDS
+  uint32_t data[kResRing][kSlotWords];
+  uint16_t srec[2 * kMaxRec];
+};
+
+// wave v's tiles: q = ntiles / nwaves each, one more for the first ntiles % nwaves waves (the
+// last-dispatched waves start latest, so they get the shorter ranges)
+__device__ __forceinline__ void res_range(const ParseParams &kp, uint32_t v, uint32_t &c0, uint32_t &c1) {
+  const uint32_t q = kp.ntiles / kp.nwaves, r = kp.ntiles % kp.nwaves;
+  c0 = v * q + (v < r ? v : r);
+  c1 = c0 + q + (v < r ? 1u : 0u);
+}
+// the wave whose range holds tile m
+__device__ __forceinline__ uint32_t res_wave_of(const ParseParams &kp, int64_t m) {
+  const uint32_t q = kp.ntiles / kp.nwaves, r = kp.ntiles % kp.nwaves;
+  const uint64_t big = (uint64_t)r * (q + 1);
+  return (uint64_t)m < big ? (uint32_t)((uint64_t)m / (q + 1)) : (uint32_t)(r + ((uint64_t)m - big) / q);
+}
+// wait until at most `ahead` tiles' DMAs are outstanding (the youngest vector-memory
+// instructions are always the DMAs of the tiles ahead, so this retires the current tile)
+__device__ __forceinline__ void res_wait(uint32_t ahead) {
+  constexpr int w1 = kDmaPer, w2 = 2 * kDmaPer;
+  if (ahead == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
+  else if (ahead == 1 || kResRing <= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (w1 & 15) | ((w1 >> 4) << 14));
+  else __builtin_amdgcn_s_waitcnt(0x0F70 | (w2 & 15) | ((w2 >> 4) << 14));
+  wave_sync();
+}
+
+// Waiting waves must not steal issue slots and memory requests from the waves still in phase A
+// (a window poll is 64 lanes x 5 granules): wait on ONE sentinel granule with a backed-off
+// s_sleep first, load whole windows only once it is there.
+__device__ __forceinline__ bool res_nap(const ParseParams &kp, uint64_t t0, uint32_t &nap) {
+  for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 clocks each
+  nap = nap < 4u ? nap * 2u : 4u;
+  if (__hip_atomic_load(kp.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kp.epoch) return false;
+  if (__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
+    __hip_atomic_store(kp.abort_word, kp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return false;
+  }
+  return true;
+}
+__device__ __forceinline__ uint64_t ld_res(uint64_t *p);
+__device__ __forceinline__ bool res_sentinel(const ParseParams &kp, uint64_t *p, uint64_t t0) {
+  uint32_t nap = 1;
+  while (!tagged(uni64(ld_res(p)), kp.epoch))
+    if (!res_nap(kp, t0, nap)) return false;
+  return true;
+}
+
+// hand-off granule read: a returning atomic (the coherent value even when this XCD's L2 holds a
+// line from an earlier poll)
+__device__ __forceinline__ uint64_t ld_res(uint64_t *p) {
+#ifdef NPR_RES_PLAIN_POLL
+  return ld_agent(p);
+#else
+  return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+}
+// one lane's element of a window: lvl 0 = wave v's A, lvl 1 = 64-wave group G1
+__device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr) {
+  LaneSeg L{};
+  L.mism = -1;
+  L.valid = true;
+  if (!inr) return L;
+  uint32_t c0, c1, d0, d1;
+  const uint32_t v0 = lvl == 0 ? (uint32_t)idx : (uint32_t)idx << 6;
+  const uint32_t v1 = lvl == 0 ? (uint32_t)idx : ((uint32_t)idx << 6) + 63u < kp.nwaves - 1 ? ((uint32_t)idx << 6) + 63u : kp.nwaves - 1;
+  res_range(kp, v0, c0, c1);
+  res_range(kp, v1, d0, d1);
+  L.first = c0;
+  L.last = (int64_t)d1 - 1;
+  const uint32_t ep = kp.epoch;
+  uint64_t *w = lvl == 0 ? kp.rslots[idx].a : kp.rgroups[idx].g;
+  const uint64_t w0 = ld_res(w + 0), w1 = ld_res(w + 1), w2 = ld_res(w + 2), w3 = ld_res(w + 3);
+  const uint64_t w4 = lvl == 0 ? w0 : ld_res(w + 4);
+  L.present = tagged(w0, ep) && tagged(w1, ep) && tagged(w2, ep) && tagged(w3, ep) && tagged(w4, ep);
+  const uint64_t e1 = w1 & kMask48;
+  L.entry = e1 ? e1 - 1 : kNone;
+  L.exit = w0 & kMask48;
+  L.cnt = w2 & kMask48;
+  if (lvl == 0) {
+    L.ok = w3 & kMask48;
+  } else {
+    const uint64_t v3 = w3 & kMask48, m = w4 & kMask48;
+    L.ok = v3 & 0xffffffffull;
+    L.valid = (v3 >> 32) & 1ull;
+    L.mism = L.valid ? -1 : (int64_t)m - 1;
+  }
+  return L;
+}
+
+// fold `cnt` (1..64) consecutive level-`lvl` elements from `base` (bounded wait for all)
+__device__ bool res_fold(const ParseParams &kp, int lvl, int64_t base, int cnt, Seg &out, uint64_t t0) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const bool inr = lane < cnt;
+  const int64_t last = base + cnt - 1;
+  if (!res_sentinel(kp, lvl == 0 ? &kp.rslots[last].a[3] : &kp.rgroups[last].g[4], t0)) return false;
+  uint32_t nap = 1;
+  for (;;) {
+    const LaneSeg L = load_res(kp, lvl, last - lane, inr);
+    if (__ballot(inr && !L.present) == 0ull) {
+      out = fold_window(kp, L, cnt - 1);
+      return true;
+    }
+    if (!res_nap(kp, t0, nap)) return false;
+  }
+}
+
+// Arrival counter: returns the count including this arrival.  Each launch counts in a bank the
+// previous resident launch zeroed (the host alternates two banks).  Callers ran
+// `s_waitcnt vmcnt(0)` after the stores the arrival vouches for.
+__device__ __forceinline__ uint32_t res_arrive(uint32_t *ctr) {
+  return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// Fold `size` children, all published: every child's exclusive prefix inside the parent (kPre*
+// words) and (lvl 0) the parent's aggregate.  lvl 0: the waves of group g -> RangeSlot e + G1(g),
+// by the group's last arrival; lvl 1: the groups -> GroupSlot e, by the last group fold (the chain-
+// consistency monoid, as fold_children does for tiles).  Read once, by returning atomics (fresh).
+__device__ void res_fold_children(const ParseParams &kp, int lvl, uint32_t g, int size) {
+  const int lane = (int)(threadIdx.x & 63u);
+  const bool inr = lane < size;
+  const int64_t c0 = lvl == 0 ? (int64_t)g << 6 : 0;
+  const LaneSeg L = load_res(kp, lvl, c0 + lane, inr);
+  const uint64_t prev_exit = shfl_up64(L.exit);
+  const bool link_bad = inr && (!L.valid || (lane > 0 && L.entry != prev_exit));
+  const bool end_mid = lane < size - 1 && L.exit < tile_end(kp, L.last);
+  Seg ep{}, agg;
+  if (__ballot(link_bad || end_mid) == 0ull) {
+    const uint32_t c = inr ? (uint32_t)L.cnt : 0u, o = inr ? (uint32_t)L.ok : 0u;
+    const uint32_t cx = excl_scan_u32(c), ox = excl_scan_u32(o);
+    ep.entry = rl64(L.entry, 0);
+    ep.exit = prev_exit;
+    ep.cnt = cx;
+    ep.ok = ox;
+    ep.valid = true;
+    ep.mism = -1;
+    agg.entry = ep.entry;
+    agg.exit = rl64(L.exit, size - 1);
+    agg.cnt = (uint32_t)__builtin_amdgcn_readlane((int)(cx + c), size - 1);
+    agg.ok = (uint32_t)__builtin_amdgcn_readlane((int)(ox + o), size - 1);
+    agg.valid = true;
+    agg.mism = -1;
+  } else {
+    const uint64_t bval = __ballot(L.valid);
+    Seg r{};
+    for (int j = 0; j < size; ++j) {
+      Seg y;
+      y.entry = rl64(L.entry, j);
+      y.exit = rl64(L.exit, j);
+      y.cnt = rl64(L.cnt, j);
+      y.ok = rl64(L.ok, j);
+      y.first = (int64_t)rl64((uint64_t)L.first, j);
+      y.last = (int64_t)rl64((uint64_t)L.last, j);
+      y.mism = (int64_t)rl64((uint64_t)L.mism, j);
+      y.valid = (bval >> j) & 1ull;
+      if (j == 0) {
+        r = y;
+      } else {
+        if (lane == j) ep = r;
+        r = combine(kp, r, y);
+      }
+    }
+    agg = r;
+  }
+  if (inr) put_prefix(kp, lvl == 0 ? kp.rslots[c0 + lane].e : kp.rgroups[lane].e, ep, lane == 0);
+  if (lvl == 0 && lane == 0) put_agg(kp, kp.rgroups + g, agg);
+}
+
+// an exclusive prefix (kPre* words) as the segment of tiles [first, last]
+__device__ __forceinline__ Seg res_prefix_seg(const ParseParams &kp, uint64_t *e, int64_t first, int64_t last,
+                                              bool &empty) {
+  const uint64_t e0 = ld_res(e + kPreExit), e1 = ld_res(e + kPreCnt), e2 = ld_res(e + kPreOk);
+  const uint64_t e3 = ld_res(e + kPreMism), e4 = ld_res(e + kPreEntry);
+  Seg s;
+  const uint64_t v = e2 & kMask48, m = e3 & kMask48, en = e4 & kMask48;
+  s.exit = e0 & kMask48;
+  s.cnt = e1 & kMask48;
+  s.ok = v & 0xffffffffull;
+  s.valid = (v >> 32) & 1ull;
+  empty = (v >> 33) & 1ull;
+  s.mism = s.valid ? -1 : (int64_t)m - 1;
+  s.entry = en ? en - 1 : kNone;
+  s.first = first;
+  s.last = last;
+  return s;
+}
+
+// the chain's anchor: `start`, or (kFlagSpecStart) the entry wave 0 speculated
+__device__ bool res_anchor(const ParseParams &kp, Seg &X, uint64_t &entry0, uint64_t t0) {
+  X = start_seg(kp);
+  entry0 = kp.start;
+  if (!(kp.flags & kFlagSpecStart)) return true;
+  for (;;) {
+    const uint64_t a1 = uni64(ld_res(&kp.rslots[0].a[1]));
+    if (tagged(a1, kp.epoch)) {
+      const uint64_t e1 = a1 & kMask48;
+      entry0 = e1 ? e1 - 1 : kNone;
+      X.entry = X.exit = e1 ? e1 - 1 : kp.stop;
+      return true;
+    }
+    if (!spin_ok(kp, t0)) return false;
+  }
+}
+
+// exact chain state before wave v (generic: contradictions settled by exact prefixes P(m))
+__device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t &entry0, uint64_t t0) {
+  const uint32_t lane = threadIdx.x & 63u;
+  if (!res_anchor(kp, X, entry0, t0)) return false;
+  const uint32_t g = v >> 6;
+  // E(g) is published by the top fold, after every group fold published its members' prefixes:
+  // one sentinel (64 pollers per granule), then two prefixes of 5 granules each
+  if (!res_sentinel(kp, &kp.rgroups[g].e[kPreEntry], t0)) return false;
+  uint32_t c0, c1, d0, d1;
+  res_range(kp, g << 6, c0, c1);
+  res_range(kp, v, d0, d1);
+  bool empty, empty2;
+  const Seg E = res_prefix_seg(kp, kp.rgroups[g].e, 0, (int64_t)c0 - 1, empty);
+  const Seg e = res_prefix_seg(kp, kp.rslots[v].e, c0, (int64_t)d0 - 1, empty2);
+  if (!empty) X = combine(kp, X, E);
+  if (!empty2) X = combine(kp, X, e);
+  if (X.valid) return true;
+  // a mis-speculated range m < v: from its exact prefix on, aggregates (G1 where aligned)
+  if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatMismWait, 1u);
+  for (;;) {
+    uint32_t a;
+    if (!X.valid) {
+      const uint32_t m = res_wave_of(kp, X.mism);
+      RangeSlot *s = kp.rslots + m;
+      uint32_t nap = 1;
+      for (;;) {
+        const uint64_t p0 = ld_res(&s->p[0]), p1 = ld_res(&s->p[1]), p2 = ld_res(&s->p[2]);
+        if (tagged(p0, kp.epoch) && tagged(p1, kp.epoch) && tagged(p2, kp.epoch)) {
+          uint32_t c0, c1;
+          res_range(kp, m, c0, c1);
+          X.exit = p0 & kMask48;
+          X.cnt = p1 & kMask48;
+          X.ok = p2 & kMask48;
+          X.first = 0;
+          X.last = (int64_t)c1 - 1;
+          X.mism = -1;
+          X.valid = true;
+          break;
+        }
+        if (!res_nap(kp, t0, nap)) return false;
+      }
+      a = m + 1;
+    } else {
+      return true;
+    }
+    while (a < v && X.valid) {
+      Seg Y;
+      if ((a & 63u) == 0 && v - a >= 64) {
+        const uint32_t ng = (v - a) >> 6;
+        if (!res_fold(kp, 1, a >> 6, (int)(ng < 64 ? ng : 64), Y, t0)) return false;
+        a += (ng < 64 ? ng : 64) << 6;
+      } else {
+        const uint32_t to_grp = 64u - (a & 63u), cnt = v - a < to_grp ? v - a : to_grp;
+        if (!res_fold(kp, 0, a, (int)cnt, Y, t0)) return false;
+        a += cnt;
+      }
+      X = combine(kp, X, Y);
+    }
+    if (X.valid) return true;
+  }
+}
+
+// one Ok flow row (+ its IPv6 side row, re-read from the capture at the decoded offset)
+__device__ __forceinline__ void res_put(const ParseParams &kp, uint64_t o, const uint32_t (&s)[8], uint64_t p) {
+  const bool v6 = (s[6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+  u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
+  d[0] = u32x4{v6 ? 0u : s[0], v6 ? 0u : s[1], s[2], s[3]};
+  d[1] = u32x4{s[4], s[5], s[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+  if (v6 && kp.flows_v6) {
+    const uint64_t a = p + 16 + s[0];  // the 32-B address block: 9 aligned dwords + alignbyte
+    const uint64_t al = a & ~3ull;
+    const uint64_t room = kp.len - al;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + al), 0, (int)(room < 36 ? room : 36), 0x00020000);
+    uint32_t x[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) x[k] = __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * k, 0, 0);
+    const uint32_t sh = (uint32_t)(a & 3u);
+    u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
+    d6[0] = u32x4{__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                  __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(x[4], x[3], sh)};
+    d6[1] = u32x4{__builtin_amdgcn_alignbyte(x[5], x[4], sh), __builtin_amdgcn_alignbyte(x[6], x[5], sh),
+                  __builtin_amdgcn_alignbyte(x[7], x[6], sh), __builtin_amdgcn_alignbyte(x[8], x[7], sh)};
+  }
+}
+
+// Re-read tiles [t0, c1) of the range from the exact chain position `pos` (counts pcnt / pok
+// before it): walk, decode, write every Ok flow.  Returns the exit; updates the counts.
+__device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_from, uint32_t c1, uint64_t pos,
+                             uint64_t &cnt, uint64_t &ok) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int k = 0; k < kResRing - 1; ++k)
+    if (t_from + k < c1) dma_tile(kp, kp.org + (uint64_t)(t_from + k) * kTile, sh.data[k]);
+  bool ended = false;
+  for (uint32_t t = t_from; t < c1; ++t) {
+    const uint32_t slot = (t - t_from) % kResRing;
+    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
+    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
+    if (t + kResRing - 1 < c1)
+      dma_tile(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.data[(slot + kResRing - 1) % kResRing]);
+    res_wait(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    const uint32_t *w = sh.data[slot];
+    if (!ended && pos >= tile_lo && pos < tile_hi) {
+      uint32_t n = 0;
+      const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n));
+      wave_sync();
+      uint32_t okbase = 0;
+      for (int s = 0; s < kRounds; ++s) {
+        if ((uint32_t)s * 64u >= n) break;
+        const uint32_t i = lane + (uint32_t)s * 64u;
+        const bool valid = i < n;
+        FlowWords f;
+        const uint32_t rel = sh.srec[i];
+        const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
+        const uint64_t bal = __ballot(okr);
+        if (okr && kp.flows) {
+          const uint64_t fi = ok + okbase + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+          if (fi < kp.flow_cap) {
+            const uint64_t o = kp.flow_cap - 1 - fi;
+            const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
+                                    f.d[4], f.d[5], f.d[6], 0u};
+            res_put(kp, o, sw, tile_lo + rel);
+          }
+        }
+        okbase += (uint32_t)__builtin_popcountll(bal);
+      }
+      cnt += n;
+      ok += okbase;
+      ended = ex < tile_hi;  // Err(Incomplete): the chain stops here (Q3)
+      pos = ex;
+    }
+    wave_sync();  // done with this slot before it is refilled
+  }
+  return pos;
+}
+
+template <bool DIAG>
+__global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ResShared sh;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t v = blockIdx.x;
+  Stamps st;
+  if (DIAG) stamp_at(st, 0);
+  uint32_t c0, c1;
+  res_range(kp, v, c0, c1);
+  const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
+  const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
+  if (v == 0) {  // zero the other counter bank for the next resident launch
+    kp.rcnt_next[16u * lane] = 0u;
+    if (lane == 0) kp.rcnt_next[16u * 64u] = 0u;
+  }
+  const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
+#pragma unroll
+  for (int k = 0; k < kResRing - 1; ++k)
+    if (c0 + k < c1) dma_tile(kp, base + (uint64_t)k * kTile, sh.data[k]);
+
+  // ---- phase A ------------------------------------------------------------------------------
+  uint32_t fl[kResSlots][8];                   // kept rounds: d[0..6] (IPv6: d[0] = address offset), record offset - base
+  uint32_t m_ok = 0, m_lo = 0, m_hi = 0;       // lane k: Ok flows before kept round k, its Ok ballot
+  uint32_t ns = 0;                             // kept rounds
+  uint64_t entry = kNone, pos = kNone;         // speculated entry; chain position
+  bool ended = false;
+  uint32_t cnt = 0, okc = 0;                   // records / Ok flows of the range (speculative chain)
+  uint32_t tdef = c1;                          // first deferred tile (its flows are re-read in phase B)
+  uint64_t pdef = 0;
+  uint32_t cdef = 0, odef = 0;
+  SpecCtx sc{};
+  for (uint32_t t = c0; t < c1; ++t) {
+    const uint32_t k = t - c0, slot = k % kResRing;
+    const uint64_t tile_lo = base + (uint64_t)k * kTile;
+    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
+    if (t + kResRing - 1 < c1)
+      dma_tile(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.data[(slot + kResRing - 1) % kResRing]);
+    res_wait(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    if (t == c0) {
+      sc = spec_ctx(kp, scb);
+      if (DIAG) stamp_at(st, 1);
+    }
+    const uint32_t *w = sh.data[slot];
+    if (!ended) {
+      if (pos == kNone) {
+        uint64_t e;
+        if (t == 0 && !spec0) {
+          e = kp.start;
+        } else {
+          const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;
+          e = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+        }
+        e = uni64(e);
+        if (e != kNone) entry = pos = e;
+      }
+      if (pos != kNone && pos < tile_hi) {
+        uint32_t n = 0;
+        const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n));
+        wave_sync();
+        const uint32_t rounds = (n + 63u) >> 6;
+        if (tdef == c1 && ns + rounds > (uint32_t)kResSlots) {  // out of registers: defer the rest
+          tdef = t;
+          pdef = pos;
+          cdef = cnt;
+          odef = okc;
+        }
+        if (tdef == c1) {
+          for (uint32_t s = 0; s < rounds; ++s) {
+            const uint32_t i = lane + s * 64u;
+            const bool valid = i < n;
+            FlowWords f;
+            const uint32_t rel = sh.srec[i];
+            const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
+            const uint64_t bal = __ballot(okr);
+            const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
+                                    f.d[4], f.d[5], f.d[6], (uint32_t)(tile_lo + rel - base)};
+#pragma unroll
+            for (int q = 0; q < kResSlots; ++q)
+              if ((uint32_t)q == ns) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) fl[q][j] = sw[j];
+              }
+            m_ok = lane == ns ? okc : m_ok;
+            m_lo = lane == ns ? (uint32_t)bal : m_lo;
+            m_hi = lane == ns ? (uint32_t)(bal >> 32) : m_hi;
+            ++ns;
+            okc += (uint32_t)__builtin_popcountll(bal);
+          }
+        } else {  // deferred: status only (the Ok count), flows re-read in phase B
+          for (uint32_t s = 0; s < rounds; ++s) {
+            const uint32_t i = lane + s * 64u;
+            const bool valid = i < n;
+            FlowWords f;
+            const bool okr = decode_rec<false>(kp, w, tile_lo, sh.srec[i], f, valid) == NPR_FLOW_OK && valid;
+            okc += (uint32_t)__builtin_popcountll(__ballot(okr));
+          }
+        }
+        cnt += n;
+        ended = ex < tile_hi;  // Err(Incomplete): the chain stops here (Q3)
+        pos = ex;
+      }
+    }
+    wave_sync();  // done with this slot before it is refilled
+  }
+  if (DIAG) stamp_at(st, 2);
+  const uint32_t ep = kp.epoch;
+  if (lane == 0) {
+    RangeSlot *rs = kp.rslots + v;
+    st_agent(&rs->a[0], gran(ep, pos == kNone ? 0ull : pos));
+    st_agent(&rs->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
+    st_agent(&rs->a[2], gran(ep, cnt));
+    st_agent(&rs->a[3], gran(ep, okc));
+  }
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // A landed before the arrival that vouches for it
+  {
+    const uint32_t g = v >> 6, gsize = kp.nwaves - (g << 6) < 64u ? kp.nwaves - (g << 6) : 64u;
+    uint32_t last = 0;
+    if (lane == 0) last = res_arrive(kp.rcnt + 16u * g) == gsize;
+    if (__builtin_amdgcn_readfirstlane(last)) {  // the group's last arrival folds it: all A's are there
+      res_fold_children(kp, 0, g, (int)gsize);
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+      const uint32_t ng = (kp.nwaves + 63u) >> 6;
+      uint32_t top = 0;
+      if (lane == 0) top = res_arrive(kp.rcnt + 16u * 64u) == ng;
+      if (__builtin_amdgcn_readfirstlane(top)) res_fold_children(kp, 1, 0, (int)ng);
+    }
+  }
+
+  // ---- phase B ------------------------------------------------------------------------------
+  if (DIAG) stamp_at(st, 3);
+  Seg X;
+  uint64_t entry0;
+  if (!res_prefix(kp, v, X, entry0, t0)) return;
+  if (DIAG) stamp_at(st, 4);
+  const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1 - 1);
+  uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
+  const bool before_end = X.exit < tile_end(kp, X.last);  // the chain ended before this range
+  if (!before_end && xe < range_hi && xe >= range_lo) {
+    if (entry != kNone && xe == entry) {  // the speculated chain is the exact one: flows from registers
+      if (kp.flows) {
+#pragma unroll
+        for (int q = 0; q < kResSlots; ++q) {
+          if ((uint32_t)q < ns) {
+            const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
+            const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
+                                 (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
+            if ((bal >> lane) & 1ull) {
+              const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+              if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
+            }
+          }
+        }
+      }
+      if (DIAG) stamp_at(st, 5);
+      if (tdef < c1) {
+        uint64_t dc = xc + cdef, dok = xo + odef;
+        (void)res_emit(kp, sh, tdef, c1, pdef, dc, dok);
+        if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - tdef);
+      }
+      xe = pos;
+      xc += cnt;
+      xo += okc;
+    } else {  // mis-speculated: re-read the whole range from the exact position
+      xe = uni64(res_emit(kp, sh, c0, c1, xe, xc, xo));
+      if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - c0);
+    }
+  }
+  if (lane == 0) {
+    RangeSlot *rs = kp.rslots + v;
+    st_agent(&rs->p[0], gran(ep, xe));
+    st_agent(&rs->p[1], gran(ep, xc));
+    st_agent(&rs->p[2], gran(ep, xo));
+    if (v == kp.nwaves - 1) {
+      uint32_t fl2 = 0;
+      if (kp.flows && xo > kp.flow_cap) fl2 |= NPR_SUMMARY_FLOW_OVERFLOW;
+      kp.summary->n_records = xc;
+      kp.summary->n_flows = xo;
+      kp.summary->consumed = xe;
+      kp.summary->flags = fl2;
+      kp.summary->entry = entry0;
+      kp.summary->epoch = ep;
+    }
+  }
+  if (DIAG) {
+    stamp_at(st, 6);
+    st.v[8] = c1 - c0;
+    st.v[9] = ns;
+    st.v[10] = c1 - tdef;
+    st.v[11] = (entry != kNone && xe == pos) ? 1 : 0;
+    stamp_flush(kp, st, v, 0xF7Fu);
+  }
+}
+
+int resident_waves_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false>), kWave, 0) !=
+      hipSuccess)
+    return 0;
+  return nb;
+}
+
 template <bool DIAG>
 static hipError_t launch(const ParseParams &p, hipStream_t s) {
   hipLaunchKernelGGL((k_count_tiles<DIAG>), dim3(p.ntiles), dim3(kWave), 0, s, p);
@@ -1268,6 +1845,11 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
 }
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
+  if (p.nwaves) {
+    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_resident<true>), dim3(p.nwaves), dim3(kWave), 0, s, p);
+    else hipLaunchKernelGGL((k_parse_resident<false>), dim3(p.nwaves), dim3(kWave), 0, s, p);
+    return hipGetLastError();
+  }
   return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
 }
 

@@ -35,16 +35,18 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     """Run the device path on `blob` and compare everything with the oracle.
 
     light requests flows only (no record table / status), so the flow table, counts and
-    `consumed` are compared.  light=True runs the parked-flow mode (pass 1 parks each
-    tile's Ok flows, pass 2 reverses them: the default); light="decode" the same launch with
-    NPR_OPT_PARK_FLOWS off (pass 2 re-decodes the records)."""
-    if light == "decode":
+    `consumed` are compared.  light=True runs the resident single pass (k_parse_resident, the
+    default for flows-only launches); light=N (an int > 1) the same with at most N waves, so
+    each wave owns a long tile range (kept-round overflow -> deferred tiles, many ranges per
+    64-wave group, speculation at range starts deep inside the capture); light="decode" the
+    two-pass kernels (NPR_OPT_RESIDENT off)."""
+    if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
         ctx = npr.context(0)
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PARK_FLOWS, 0))
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
         try:
             return check_parity(blob, start, endianness, ws, light=True)
         finally:
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PARK_FLOWS, 1))
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
     if start == 24:
         rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
         assert rc == 0
@@ -116,7 +118,8 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-LIGHT = pytest.mark.parametrize("light", [False, True, "decode"], ids=["full", "flows_only", "flows_only_decode"])
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, "decode"],
+                                ids=["full", "resident", "resident_w7", "resident_w100", "two_pass"])
 
 
 @LIGHT
