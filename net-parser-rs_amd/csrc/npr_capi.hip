@@ -45,8 +45,10 @@ struct npr_ctx {
 
 namespace {
 
-// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each)
-constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlBytes = kCtlCounters + 2 * kCtlBank;
+// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each),
+// per-workgroup ready granules (64 B apart)
+constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlFlags = kCtlCounters + 2 * kCtlBank,
+                 kCtlBytes = kCtlFlags + (npr::kResMaxWaves / npr::kResWgMin) * 64;
 constexpr uint32_t kTimeoutTicks = 100u * 1000u * 1000u;  // 1 s of s_memrealtime (100 MHz)
 
 npr_status fail(npr_ctx *c, npr_status st, const char *fmt, ...) {
@@ -347,6 +349,7 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
     const uint64_t bank = c->res_launches++ & 1u;  // this launch counts in a bank the previous one zeroed
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters + bank * kCtlBank);
     p.rcnt_next = (uint32_t *)((char *)c->abort_word + kCtlCounters + (bank ^ 1u) * kCtlBank);
+    p.rready = (uint64_t *)((char *)c->abort_word + kCtlFlags);
   }
   HIP_CHECK(c, npr::launch_parse_extract(p, s));
   return NPR_OK;

@@ -53,7 +53,8 @@ struct alignas(128) RangeSlot {
   uint64_t pad[4];
 };
 static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
-constexpr uint32_t kResMaxWaves = 64 * 64;  // two fold levels: 64 groups of 64 waves
+constexpr uint32_t kResMaxWaves = 64 * 64;  // at most 4096 persistent waves
+constexpr uint32_t kResWgMin = 16;          // waves per workgroup (npr_kernels.hip kResWg) is at least this
 
 // exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
 enum : int { kPreExit = 0, kPreCnt = 1, kPreOk = 2, kPreMism = 3, kPreEntry = 4 };
@@ -108,6 +109,7 @@ struct ParseParams {
   GroupSlot *rgroups;      // [ceil(nwaves / 64)]
   uint32_t *rcnt;          // arrival counters (zero at launch): group g at [16 g], the group folds at [16 * 64]
   uint32_t *rcnt_next;     // the other bank: zeroed by this launch for the next resident launch
+  uint64_t *rready;        // per-workgroup ready granule (8 words apart): every G(b) published
 };
 
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)

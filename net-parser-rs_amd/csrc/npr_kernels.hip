@@ -505,13 +505,15 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
 }
 // exclusive prefix sum over the 64 lanes (every lane active)
 __device__ __forceinline__ uint32_t excl_scan_u32(uint32_t v) {
-  const int lane = (int)(threadIdx.x & 63u);
+  // inclusive scan by DPP: row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15 / :31
+  // carry the row totals (no LDS round trips)
   uint32_t x = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, (unsigned)o, 64);
-    if (lane >= o) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);
   return x - v;
 }
 // whole-wave sum (DPP reduction of the device library); every lane must be active
@@ -1253,7 +1255,6 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
       kp.summary->n_flows = nok;
       kp.summary->consumed = ex;
       kp.summary->flags = fl;
-      kp.summary->entry = entry0;
       kp.summary->epoch = kp.epoch;
     }
   }
@@ -1289,6 +1290,11 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
 constexpr int kResSlots = NPR_RES_SLOTS;  // 64-record rounds of flows held in registers per wave
 constexpr int kResRing = NPR_RES_RING;    // LDS tile slots per wave (1 processed + kResRing-1 in flight)
 constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
+#ifndef NPR_RES_WG
+#define NPR_RES_WG 16
+#endif
+constexpr uint32_t kResWg = NPR_RES_WG;   // waves per workgroup (one workgroup per CU): folded in LDS
+static_assert(kResWg >= kResWgMin, "ready granules are sized for kResWgMin");
 static_assert(kResRing >= 2 && (kResRing - 1) * kDmaPer < 64, "vmcnt field is 6 bits");
 
 struct ResShared {  // one wave's LDS
@@ -1324,7 +1330,7 @@ __device__ __forceinline__ void res_wait(uint32_t ahead) {
 // s_sleep first, load whole windows only once it is there.
 __device__ __forceinline__ bool res_nap(const ParseParams &kp, uint64_t t0, uint32_t &nap) {
   for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 clocks each
-  nap = nap < 4u ? nap * 2u : 4u;
+  nap = nap < 2u ? nap * 2u : 2u;
   if (__hip_atomic_load(kp.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kp.epoch) return false;
   if (__builtin_amdgcn_s_memrealtime() - t0 > kp.timeout_ticks) {
     __hip_atomic_store(kp.abort_word, kp.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1349,23 +1355,29 @@ __device__ __forceinline__ uint64_t ld_res(uint64_t *p) {
   return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #endif
 }
-// one lane's element of a window: lvl 0 = wave v's A, lvl 1 = 64-wave group G1
-__device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr) {
+// one lane's element of a window: lvl 0 = wave v's A, lvl 1 = workgroup b's aggregate G(b)
+__device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr, bool sc1 = false) {
   LaneSeg L{};
   L.mism = -1;
   L.valid = true;
   if (!inr) return L;
   uint32_t c0, c1, d0, d1;
-  const uint32_t v0 = lvl == 0 ? (uint32_t)idx : (uint32_t)idx << 6;
-  const uint32_t v1 = lvl == 0 ? (uint32_t)idx : ((uint32_t)idx << 6) + 63u < kp.nwaves - 1 ? ((uint32_t)idx << 6) + 63u : kp.nwaves - 1;
+  const uint32_t v0 = lvl == 0 ? (uint32_t)idx : (uint32_t)idx * kResWg;
+  const uint32_t v1 = lvl == 0 ? (uint32_t)idx : v0 + kResWg - 1u < kp.nwaves - 1 ? v0 + kResWg - 1u : kp.nwaves - 1;
   res_range(kp, v0, c0, c1);
   res_range(kp, v1, d0, d1);
   L.first = c0;
   L.last = (int64_t)d1 - 1;
   const uint32_t ep = kp.epoch;
   uint64_t *w = lvl == 0 ? kp.rslots[idx].a : kp.rgroups[idx].g;
-  const uint64_t w0 = ld_res(w + 0), w1 = ld_res(w + 1), w2 = ld_res(w + 2), w3 = ld_res(w + 3);
-  const uint64_t w4 = lvl == 0 ? w0 : ld_res(w + 4);
+  uint64_t w0, w1, w2, w3, w4;
+  if (sc1) {  // sc1 loads: fast, but may hit a stale line (the tags tell; callers re-read those)
+    w0 = ld_agent(w + 0), w1 = ld_agent(w + 1), w2 = ld_agent(w + 2), w3 = ld_agent(w + 3);
+    w4 = lvl == 0 ? w0 : ld_agent(w + 4);
+  } else {
+    w0 = ld_res(w + 0), w1 = ld_res(w + 1), w2 = ld_res(w + 2), w3 = ld_res(w + 3);
+    w4 = lvl == 0 ? w0 : ld_res(w + 4);
+  }
   L.present = tagged(w0, ep) && tagged(w1, ep) && tagged(w2, ep) && tagged(w3, ep) && tagged(w4, ep);
   const uint64_t e1 = w1 & kMask48;
   L.entry = e1 ? e1 - 1 : kNone;
@@ -1406,19 +1418,16 @@ __device__ __forceinline__ uint32_t res_arrive(uint32_t *ctr) {
   return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 }
 
-// Fold `size` children, all published: every child's exclusive prefix inside the parent (kPre*
-// words) and (lvl 0) the parent's aggregate.  lvl 0: the waves of group g -> RangeSlot e + G1(g),
-// by the group's last arrival; lvl 1: the groups -> GroupSlot e, by the last group fold (the chain-
-// consistency monoid, as fold_children does for tiles).  Read once, by returning atomics (fresh).
-__device__ void res_fold_children(const ParseParams &kp, int lvl, uint32_t g, int size) {
+// Fold a window of `size` children held one per lane (ascending lane = ascending order): each
+// lane's exclusive prefix inside the window (lane 0: none) and the window's aggregate (the chain-
+// consistency monoid; fast path: every link consistent -> two exclusive scans).
+__device__ void res_fold_lanes(const ParseParams &kp, const LaneSeg &L, int size, Seg &ep, Seg &agg) {
   const int lane = (int)(threadIdx.x & 63u);
   const bool inr = lane < size;
-  const int64_t c0 = lvl == 0 ? (int64_t)g << 6 : 0;
-  const LaneSeg L = load_res(kp, lvl, c0 + lane, inr);
   const uint64_t prev_exit = shfl_up64(L.exit);
   const bool link_bad = inr && (!L.valid || (lane > 0 && L.entry != prev_exit));
   const bool end_mid = lane < size - 1 && L.exit < tile_end(kp, L.last);
-  Seg ep{}, agg;
+  ep = Seg{};
   if (__ballot(link_bad || end_mid) == 0ull) {
     const uint32_t c = inr ? (uint32_t)L.cnt : 0u, o = inr ? (uint32_t)L.ok : 0u;
     const uint32_t cx = excl_scan_u32(c), ox = excl_scan_u32(o);
@@ -1426,12 +1435,16 @@ __device__ void res_fold_children(const ParseParams &kp, int lvl, uint32_t g, in
     ep.exit = prev_exit;
     ep.cnt = cx;
     ep.ok = ox;
+    ep.first = (int64_t)rl64((uint64_t)L.first, 0);
+    ep.last = (int64_t)shfl_up64((uint64_t)L.last);
     ep.valid = true;
     ep.mism = -1;
     agg.entry = ep.entry;
     agg.exit = rl64(L.exit, size - 1);
     agg.cnt = (uint32_t)__builtin_amdgcn_readlane((int)(cx + c), size - 1);
     agg.ok = (uint32_t)__builtin_amdgcn_readlane((int)(ox + o), size - 1);
+    agg.first = ep.first;
+    agg.last = (int64_t)rl64((uint64_t)L.last, size - 1);
     agg.valid = true;
     agg.mism = -1;
   } else {
@@ -1456,9 +1469,9 @@ __device__ void res_fold_children(const ParseParams &kp, int lvl, uint32_t g, in
     }
     agg = r;
   }
-  if (inr) put_prefix(kp, lvl == 0 ? kp.rslots[c0 + lane].e : kp.rgroups[lane].e, ep, lane == 0);
-  if (lvl == 0 && lane == 0) put_agg(kp, kp.rgroups + g, agg);
 }
+
+constexpr int kTopWin = (int)((kResMaxWaves / kResWg + 63) / 64);  // windows of workgroup aggregates
 
 // an exclusive prefix (kPre* words) as the segment of tiles [first, last]
 __device__ __forceinline__ Seg res_prefix_seg(const ParseParams &kp, uint64_t *e, int64_t first, int64_t last,
@@ -1479,39 +1492,10 @@ __device__ __forceinline__ Seg res_prefix_seg(const ParseParams &kp, uint64_t *e
   return s;
 }
 
-// the chain's anchor: `start`, or (kFlagSpecStart) the entry wave 0 speculated
-__device__ bool res_anchor(const ParseParams &kp, Seg &X, uint64_t &entry0, uint64_t t0) {
-  X = start_seg(kp);
-  entry0 = kp.start;
-  if (!(kp.flags & kFlagSpecStart)) return true;
-  for (;;) {
-    const uint64_t a1 = uni64(ld_res(&kp.rslots[0].a[1]));
-    if (tagged(a1, kp.epoch)) {
-      const uint64_t e1 = a1 & kMask48;
-      entry0 = e1 ? e1 - 1 : kNone;
-      X.entry = X.exit = e1 ? e1 - 1 : kp.stop;
-      return true;
-    }
-    if (!spin_ok(kp, t0)) return false;
-  }
-}
-
-// exact chain state before wave v (generic: contradictions settled by exact prefixes P(m))
-__device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t &entry0, uint64_t t0) {
+// exact chain state before wave v, from X = E(b) ⊕ (prefix inside the workgroup) when that is
+// flagged: contradictions settled by exact prefixes P(m), then aggregates (G(b) where aligned)
+__device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t0) {
   const uint32_t lane = threadIdx.x & 63u;
-  if (!res_anchor(kp, X, entry0, t0)) return false;
-  const uint32_t g = v >> 6;
-  // E(g) is published by the top fold, after every group fold published its members' prefixes:
-  // one sentinel (64 pollers per granule), then two prefixes of 5 granules each
-  if (!res_sentinel(kp, &kp.rgroups[g].e[kPreEntry], t0)) return false;
-  uint32_t c0, c1, d0, d1;
-  res_range(kp, g << 6, c0, c1);
-  res_range(kp, v, d0, d1);
-  bool empty, empty2;
-  const Seg E = res_prefix_seg(kp, kp.rgroups[g].e, 0, (int64_t)c0 - 1, empty);
-  const Seg e = res_prefix_seg(kp, kp.rslots[v].e, c0, (int64_t)d0 - 1, empty2);
-  if (!empty) X = combine(kp, X, E);
-  if (!empty2) X = combine(kp, X, e);
   if (X.valid) return true;
   // a mis-speculated range m < v: from its exact prefix on, aggregates (G1 where aligned)
   if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatMismWait, 1u);
@@ -1543,12 +1527,12 @@ __device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t &
     }
     while (a < v && X.valid) {
       Seg Y;
-      if ((a & 63u) == 0 && v - a >= 64) {
-        const uint32_t ng = (v - a) >> 6;
-        if (!res_fold(kp, 1, a >> 6, (int)(ng < 64 ? ng : 64), Y, t0)) return false;
-        a += (ng < 64 ? ng : 64) << 6;
+      if (a % kResWg == 0 && v - a >= kResWg) {
+        const uint32_t ng = (v - a) / kResWg, take = ng < 64 ? ng : 64;
+        if (!res_fold(kp, 1, a / kResWg, (int)take, Y, t0)) return false;
+        a += take * kResWg;
       } else {
-        const uint32_t to_grp = 64u - (a & 63u), cnt = v - a < to_grp ? v - a : to_grp;
+        const uint32_t to_grp = kResWg - a % kResWg, cnt = v - a < to_grp ? v - a : to_grp;
         if (!res_fold(kp, 0, a, (int)cnt, Y, t0)) return false;
         a += cnt;
       }
@@ -1633,25 +1617,37 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
   return pos;
 }
 
+struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS fold
+  ResShared w[kResWg];
+  Seg a[kResWg];   // each wave's range aggregate A
+  Seg x[kResWg];   // each wave's prefix: anchor ⊕ G(0..b-1) ⊕ A(waves before it here)
+  uint32_t fail;   // a bounded wait of wave 0 timed out: every wave leaves
+};
+
 template <bool DIAG>
-__global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ResShared sh;
+__global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ResWgShared sh;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t v = blockIdx.x;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar LDS bases
+  const uint32_t b = blockIdx.x, v = b * kResWg + wid;
+  const uint32_t nb = (kp.nwaves + kResWg - 1) / kResWg;
+  const uint32_t nw = kp.nwaves - b * kResWg < kResWg ? kp.nwaves - b * kResWg : kResWg;  // waves of this workgroup
+  const bool active = wid < nw;
   Stamps st;
   if (DIAG) stamp_at(st, 0);
-  uint32_t c0, c1;
-  res_range(kp, v, c0, c1);
+  uint32_t c0 = 0, c1 = 0;
+  if (active) res_range(kp, v, c0, c1);
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
   const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
   if (v == 0) {  // zero the other counter bank for the next resident launch
     kp.rcnt_next[16u * lane] = 0u;
     if (lane == 0) kp.rcnt_next[16u * 64u] = 0u;
   }
+  if (threadIdx.x == 0) sh.fail = 0;
   const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
 #pragma unroll
   for (int k = 0; k < kResRing - 1; ++k)
-    if (c0 + k < c1) dma_tile(kp, base + (uint64_t)k * kTile, sh.data[k]);
+    if (c0 + k < c1) dma_tile(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
 
   // ---- phase A ------------------------------------------------------------------------------
   uint32_t fl[kResSlots][8];                   // kept rounds: d[0..6] (IPv6: d[0] = address offset), record offset - base
@@ -1669,13 +1665,13 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     if (t + kResRing - 1 < c1)
-      dma_tile(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.data[(slot + kResRing - 1) % kResRing]);
+      dma_tile(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
     res_wait(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
     if (t == c0) {
       sc = spec_ctx(kp, scb);
       if (DIAG) stamp_at(st, 1);
     }
-    const uint32_t *w = sh.data[slot];
+    const uint32_t *w = sh.w[wid].data[slot];
     if (!ended) {
       if (pos == kNone) {
         uint64_t e;
@@ -1690,7 +1686,7 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
       }
       if (pos != kNone && pos < tile_hi) {
         uint32_t n = 0;
-        const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n));
+        const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n));
         wave_sync();
         const uint32_t rounds = (n + 63u) >> 6;
         if (tdef == c1 && ns + rounds > (uint32_t)kResSlots) {  // out of registers: defer the rest
@@ -1704,7 +1700,7 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
             const uint32_t i = lane + s * 64u;
             const bool valid = i < n;
             FlowWords f;
-            const uint32_t rel = sh.srec[i];
+            const uint32_t rel = sh.w[wid].srec[i];
             const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
             const uint64_t bal = __ballot(okr);
             const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
@@ -1726,7 +1722,7 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
             const uint32_t i = lane + s * 64u;
             const bool valid = i < n;
             FlowWords f;
-            const bool okr = decode_rec<false>(kp, w, tile_lo, sh.srec[i], f, valid) == NPR_FLOW_OK && valid;
+            const bool okr = decode_rec<false>(kp, w, tile_lo, sh.w[wid].srec[i], f, valid) == NPR_FLOW_OK && valid;
             okc += (uint32_t)__builtin_popcountll(__ballot(okr));
           }
         }
@@ -1739,34 +1735,107 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
   }
   if (DIAG) stamp_at(st, 2);
   const uint32_t ep = kp.epoch;
-  if (lane == 0) {
+  if (active && lane == 0) {  // A: in LDS for the workgroup fold, in HBM for the rare generic prefix
     RangeSlot *rs = kp.rslots + v;
     st_agent(&rs->a[0], gran(ep, pos == kNone ? 0ull : pos));
     st_agent(&rs->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
     st_agent(&rs->a[2], gran(ep, cnt));
     st_agent(&rs->a[3], gran(ep, okc));
+    Seg A;
+    A.entry = entry;
+    A.exit = pos == kNone ? 0ull : pos;
+    A.cnt = cnt;
+    A.ok = okc;
+    A.first = c0;
+    A.last = (int64_t)c1 - 1;
+    A.mism = -1;
+    A.valid = true;
+    sh.a[wid] = A;
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // A landed before the arrival that vouches for it
-  {
-    const uint32_t g = v >> 6, gsize = kp.nwaves - (g << 6) < 64u ? kp.nwaves - (g << 6) : 64u;
-    uint32_t last = 0;
-    if (lane == 0) last = res_arrive(kp.rcnt + 16u * g) == gsize;
-    if (__builtin_amdgcn_readfirstlane(last)) {  // the group's last arrival folds it: all A's are there
-      res_fold_children(kp, 0, g, (int)gsize);
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-      const uint32_t ng = (kp.nwaves + 63u) >> 6;
-      uint32_t top = 0;
-      if (lane == 0) top = res_arrive(kp.rcnt + 16u * 64u) == ng;
-      if (__builtin_amdgcn_readfirstlane(top)) res_fold_children(kp, 1, 0, (int)ng);
+  __syncthreads();
+  if (wid == 0) {
+    // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
+    // flows wait there, so the windows get the registers.
+    static_assert(kResSlots * 8 * 64 * 4 <= 2 * sizeof(ResShared), "stash fits two rings");
+    uint32_t *stash = &sh.w[0].data[0][0];
+#pragma unroll
+    for (int q = 0; q < kResSlots; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) stash[(q * 8 + j) * 64 + lane] = fl[q][j];
+    // (1) the workgroup's waves, one per lane, from LDS: prefixes inside the workgroup + G(b)
+    LaneSeg L{};
+    if ((uint32_t)lane < nw) {
+      const Seg &A = sh.a[lane];
+      L.entry = A.entry;
+      L.exit = A.exit;
+      L.cnt = A.cnt;
+      L.ok = A.ok;
+      L.first = A.first;
+      L.last = A.last;
+      L.mism = -1;
+      L.valid = true;
+      L.present = true;
     }
+    Seg e, agg;
+    res_fold_lanes(kp, L, (int)nw, e, agg);
+    if (lane == 0) put_agg(kp, kp.rgroups + b, agg);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // A's and G(b) landed before the arrival that vouches for them
+    uint32_t last = 0;
+    if (lane == 0) last = res_arrive(kp.rcnt + 16u * 64u) == nb;
+    if (__builtin_amdgcn_readfirstlane(last)) {  // the last arrival tells every workgroup, one granule each
+#pragma unroll
+      for (uint32_t k = 0; k < kResMaxWaves / kResWgMin; k += 64)
+        if (k + lane < nb) st_agent(kp.rready + 8u * (k + lane), gran(ep, 1));
+    }
+    if (DIAG) stamp_at(st, 3);
+    // (2) every G published (this workgroup's ready granule: a returning-atomic poll, one poller per
+    //     granule), then E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1): all windows in one round trip
+    const bool okw = res_sentinel(kp, kp.rready + 8u * b, t0);
+    Seg E = start_seg(kp);
+    uint64_t entry0 = kp.start;
+    if (okw) {
+      LaneSeg G[kTopWin];
+#pragma unroll
+      for (int w = 0; w < kTopWin; ++w) {  // descending inside a window (fold_window's order)
+        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+        G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
+      }
+#pragma unroll
+      for (int w = 0; w < kTopWin; ++w) {  // a line an earlier launch left in this XCD's L2: re-read fresh
+        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+        if (__ballot((uint32_t)lane < sz && !G[w].present))
+          G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz);
+      }
+      if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
+        entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
+        E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
+      }
+#pragma unroll
+      for (int w = 0; w < kTopWin; ++w) {
+        const uint32_t w0 = 64u * (uint32_t)w;
+        if (w0 >= b) break;
+        E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
+      }
+    }
+    // (3) each wave's prefix
+    if ((uint32_t)lane < nw) sh.x[lane] = lane == 0 ? E : combine(kp, E, e);
+    if (lane == 0) {
+      sh.fail = okw ? 0u : 1u;
+      if (b == nb - 1) kp.summary->entry = entry0;
+    }
+    wave_sync();
+#pragma unroll
+    for (int q = 0; q < kResSlots; ++q)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fl[q][j] = stash[(q * 8 + j) * 64 + lane];
   }
+  __syncthreads();
+  if (!active || sh.fail) return;
 
   // ---- phase B ------------------------------------------------------------------------------
-  if (DIAG) stamp_at(st, 3);
-  Seg X;
-  uint64_t entry0;
-  if (!res_prefix(kp, v, X, entry0, t0)) return;
+  Seg X = sh.x[wid];
+  if (!X.valid && !res_prefix(kp, v, X, t0)) return;
   if (DIAG) stamp_at(st, 4);
   const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1 - 1);
   uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
@@ -1790,14 +1859,14 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
       if (DIAG) stamp_at(st, 5);
       if (tdef < c1) {
         uint64_t dc = xc + cdef, dok = xo + odef;
-        (void)res_emit(kp, sh, tdef, c1, pdef, dc, dok);
+        (void)res_emit(kp, sh.w[wid], tdef, c1, pdef, dc, dok);
         if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - tdef);
       }
       xe = pos;
       xc += cnt;
       xo += okc;
     } else {  // mis-speculated: re-read the whole range from the exact position
-      xe = uni64(res_emit(kp, sh, c0, c1, xe, xc, xo));
+      xe = uni64(res_emit(kp, sh.w[wid], c0, c1, xe, xc, xo));
       if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - c0);
     }
   }
@@ -1813,7 +1882,6 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
       kp.summary->n_flows = xo;
       kp.summary->consumed = xe;
       kp.summary->flags = fl2;
-      kp.summary->entry = entry0;
       kp.summary->epoch = ep;
     }
   }
@@ -1829,10 +1897,10 @@ __global__ __launch_bounds__(kWave) void k_parse_resident(ParseParams kp) {
 
 int resident_waves_per_cu() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false>), kWave, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false>), kResWg * kWave, 0) !=
       hipSuccess)
     return 0;
-  return nb;
+  return nb * (int)kResWg;
 }
 
 template <bool DIAG>
@@ -1846,8 +1914,9 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
   if (p.nwaves) {
-    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_resident<true>), dim3(p.nwaves), dim3(kWave), 0, s, p);
-    else hipLaunchKernelGGL((k_parse_resident<false>), dim3(p.nwaves), dim3(kWave), 0, s, p);
+    const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
+    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_resident<true>), dim3(nb), dim3(kResWg * kWave), 0, s, p);
+    else hipLaunchKernelGGL((k_parse_resident<false>), dim3(nb), dim3(kResWg * kWave), 0, s, p);
     return hipGetLastError();
   }
   return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
