@@ -279,7 +279,11 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
 #pragma unroll
   for (int k = 0; k < 17; ++k) asm volatile("" : "+v"(a[k]));
   auto byte = [&](int i) { return (a[i >> 2] >> (8 * (i & 3))) & 0xffu; };
-  auto be16 = [&](int i) { return (byte(i) << 8) | byte(i + 1); };
+  // big-endian u16 at byte i: one v_perm_b32 over the two words that may hold it
+  auto be16 = [&](int i) {
+    const int k = i >> 2, k1 = k + 1 < 17 ? k + 1 : 16;
+    return __builtin_amdgcn_perm(a[k1], a[k], 0x0c0c0000u | ((uint32_t)(i & 3) << 8) | (uint32_t)((i & 3) + 1));
+  };
   // Every quantity is computed for every lane and combined by selects (no data-dependent
   // branches: divergent if/else here costs more scalar exec-mask work than the arithmetic).
   const uint32_t etype = be16(12), b0 = byte(14);
@@ -824,6 +828,17 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
       continue;
     }
     const uint32_t stride = 16u + incl;
+    if (span - r <= 64u * stride) {  // one header per lane reaches the tile's end: a single read
+      const uint32_t q0 = r + lane * stride;
+      uint32_t h0 = hdr(w, q0 < span ? q0 : 0u, 2, big);
+      asm volatile("" : "+v"(h0));
+      const uint64_t b0 = __ballot((lane == 0) | ((q0 < span) & (h0 == incl) & (avail - q0 >= stride)));
+      const uint32_t m = (~b0 == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~b0);
+      srec[n + lane] = (uint16_t)q0;
+      n += m;
+      p += (uint64_t)m * stride;
+      continue;
+    }
     uint64_t b[kWalkUnroll];
     uint32_t qr[kWalkUnroll];
     uint32_t h[kWalkUnroll];
@@ -1255,6 +1270,7 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
       kp.summary->n_flows = nok;
       kp.summary->consumed = ex;
       kp.summary->flags = fl;
+      kp.summary->entry = entry0;
       kp.summary->epoch = kp.epoch;
     }
   }
@@ -1705,9 +1721,10 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
             const uint64_t bal = __ballot(okr);
             const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
                                     f.d[4], f.d[5], f.d[6], (uint32_t)(tile_lo + rel - base)};
+            const uint32_t nsu = __builtin_amdgcn_readfirstlane(ns);  // uniform: one scalar branch per slot
 #pragma unroll
             for (int q = 0; q < kResSlots; ++q)
-              if ((uint32_t)q == ns) {
+              if ((uint32_t)q == nsu) {
 #pragma unroll
                 for (int j = 0; j < 8; ++j) fl[q][j] = sw[j];
               }
