@@ -1,8 +1,9 @@
 """bench.py — device-resident record parse + extract_flow (+ convert_records) on MI355X.
 
-One "step" = one launch of the fused HIP kernel over one capture already resident in HBM:
-CaptureFile::parse (record chain) + extract_flow for every record + convert_records (Ok flows,
-reverse order), i.e. the reference's `extract` bench (benches/benches.rs:40-74).
+One "step" = one launch of the resident single-pass HIP kernel (k_parse_resident) over one capture
+already resident in HBM: CaptureFile::parse (record chain) + extract_flow for every record +
+convert_records (Ok flows, reverse order), i.e. the reference's `extract` bench
+(benches/benches.rs:40-74).
 
 Workload (BASELINE.json configs[1], "C2"): 1,000,000 synthetic 64-B Ethernet/IPv4/TCP records per
 GPU (80,000,024 B capture).  N > 1: one process per GPU, each parses its own 1M-record shard
