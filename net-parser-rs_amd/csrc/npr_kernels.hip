@@ -1664,6 +1664,9 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
 #pragma unroll
   for (int k = 0; k < kResRing - 1; ++k)
     if (c0 + k < c1) dma_tile(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
+#ifndef NPR_EXP_NOPRIO
+  __builtin_amdgcn_s_setprio(3);  // lowered by one per tile parsed (below)
+#endif
 
   // ---- phase A ------------------------------------------------------------------------------
   uint32_t fl[kResSlots][8];                   // kept rounds: d[0..6] (IPv6: d[0] = address offset), record offset - base
@@ -1749,6 +1752,13 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       }
     }
     wave_sync();  // done with this slot before it is refilled
+#ifndef NPR_EXP_NOPRIO
+    // keep the CU's 16 waves in step: the SIMD arbiter favours older waves, which would finish
+    // their ranges several us before the younger ones (and the workgroup waits for its last)
+    if (k == 0) __builtin_amdgcn_s_setprio(2);
+    else if (k == 1) __builtin_amdgcn_s_setprio(1);
+    else if (k == 2) __builtin_amdgcn_s_setprio(0);
+#endif
   }
   if (DIAG) stamp_at(st, 2);
   const uint32_t ep = kp.epoch;
@@ -1796,8 +1806,9 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     }
     Seg e, agg;
     res_fold_lanes(kp, L, (int)nw, e, agg);
+    // G(b), then the arrival.  No store drain in between: readers check the granules' tags and
+    // re-read (returning atomics) until they are this launch's
     if (lane == 0) put_agg(kp, kp.rgroups + b, agg);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // A's and G(b) landed before the arrival that vouches for them
     uint32_t last = 0;
     if (lane == 0) last = res_arrive(kp.rcnt + 16u * 64u) == nb;
     if (__builtin_amdgcn_readfirstlane(last)) {  // the last arrival tells every workgroup, one granule each
@@ -1808,7 +1819,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     if (DIAG) stamp_at(st, 3);
     // (2) every G published (this workgroup's ready granule: a returning-atomic poll, one poller per
     //     granule), then E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1): all windows in one round trip
-    const bool okw = res_sentinel(kp, kp.rready + 8u * b, t0);
+    bool okw = res_sentinel(kp, kp.rready + 8u * b, t0);
     Seg E = start_seg(kp);
     uint64_t entry0 = kp.start;
     if (okw) {
@@ -1819,10 +1830,16 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
       }
 #pragma unroll
-      for (int w = 0; w < kTopWin; ++w) {  // a line an earlier launch left in this XCD's L2: re-read fresh
+      for (int w = 0; w < kTopWin; ++w) {  // not landed yet, or a line an earlier launch left in this XCD's L2
         const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-        if (__ballot((uint32_t)lane < sz && !G[w].present))
+        uint32_t nap = 1;
+        for (int tries = 0; __ballot((uint32_t)lane < sz && !G[w].present); ++tries) {
+          if (tries && !res_nap(kp, t0, nap)) {
+            okw = false;
+            break;
+          }
           G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz);
+        }
       }
       if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
         entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
@@ -1831,7 +1848,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
 #pragma unroll
       for (int w = 0; w < kTopWin; ++w) {
         const uint32_t w0 = 64u * (uint32_t)w;
-        if (w0 >= b) break;
+        if (w0 >= b || !okw) break;
         E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
       }
     }

@@ -18,3 +18,10 @@ for k, nm in [(0, "start"), (1, "landed"), (2, "A done"), (3, "published"), (4, 
     print(f"{nm:10s} {pc(S(k))}")
 for a, b, nm in [(0, 1, "first land"), (1, 2, "phase A"), (2, 3, "pub+fold"), (3, 4, "prefix wait"), (4, 6, "write")]:
     print(f"{nm:10s} {pc(S(b) - S(a))}")
+w0 = np.arange(0, nw, 16)
+if len(w0):
+    A = S(2)
+    amax = np.array([A[i:i + 16].max() for i in w0])
+    print("workgroup wave 0 (last A in the workgroup = 0):")
+    for k, nm in [(3, "arrived"), (12, "ready seen"), (13, "G landed"), (14, "E folded"), (4, "prefix")]:
+        print(f"  {nm:10s} {pc(S(k)[w0] - amax.max())}   (rel. to the last A of the launch)")
