@@ -73,8 +73,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--records", type=int, default=1_000_000)
-    ap.add_argument("--copies", type=int, default=4)
+    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
+                    help="c2 (the headline: 1M x 64-B records) or c3 (8M records, frames U[64,1500], ~6.4 GB; "
+                         "parsed as chained ~80 MB launches)")
+    ap.add_argument("--records", type=int, default=None)
+    ap.add_argument("--copies", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
@@ -88,10 +91,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    n = args.records
-    blob = synth.fixed64(n)  # same capture on every rank: each GPU parses its own 1M-record shard
+    c3 = args.config == "c3"
+    n = args.records or (8_000_000 if c3 else 1_000_000)
+    copies = args.copies or (1 if c3 else 4)
+    # same capture on every rank: each GPU parses its own shard
+    blob = synth.variable_mix(n) if c3 else synth.fixed64(n)
     host = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
-    bufs = [host.to(dev) for _ in range(args.copies)]
+    bufs = [host.to(dev) for _ in range(copies)]
     hdr = npr.GlobalHeader.parse(blob[:24])[1]
     ws = device.Workspace(record_cap=n, flow_cap=n, device=local, records=False, offsets=False, status=False,
                           flows=True, flows_v6=True)
@@ -101,10 +107,12 @@ def main():
     # correctness gate for the measured configuration
     ws.launch(bufs[0], start=24, endianness=hdr.endianness)
     sm = ws.check()
-    assert sm.n_records == n and sm.n_flows == n and sm.consumed == len(blob), (sm.n_records, sm.n_flows)
+    # C2: every record is an Ok flow; C3: short TCP frames with a long data offset are not (Q9)
+    assert sm.n_records == n and sm.consumed == len(blob) and (sm.n_flows == n or c3), (sm.n_records, sm.n_flows)
+    n_flows = int(sm.n_flows)
 
     for i in range(args.warmup):
-        ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
+        ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
     torch.cuda.synchronize()
 
     # ONE event pair brackets the K launches on their stream (per-step events would add marker
@@ -116,21 +124,21 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for i in range(args.steps):
-        ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
+        ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
     ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
     sm = ws.check()
-    assert sm.n_records == n and sm.n_flows == n
+    assert sm.n_records == n and sm.n_flows == n_flows
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # average launch (scan + emit) on the device
     if args.stats:
         import ctypes
         lib, h = ws.ctx.lib, ws.ctx.handle
         ws.ctx.check(lib.npr_ctx_set_stats(h, 2))
         for i in range(3):
-            ws.launch(bufs[i % args.copies], start=24, endianness=hdr.endianness)
+            ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
         ws.check()
         st = (ctypes.c_uint32 * 8)()
         ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
@@ -154,11 +162,12 @@ def main():
         total_records = n * world * args.steps
         value = total_records / wall / 1e6
         stream_bytes = len(blob) - 24                       # sum(16 + incl_len) per capture
-        read_b = len(blob)                                  # every byte of the capture is read
-        write_b = 32 * n                                    # one 32-B npr_flow per Ok record
+        read_b = len(blob)                                  # every byte of the capture is read (C2:
+        # = SURVEY 8d's 16 + min(incl, 64) per record; C3: the tiles stream whole payloads too)
+        write_b = 32 * n_flows                              # one 32-B npr_flow per Ok record
         alg = read_b + write_b
         achieved = alg / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(n)
+        traffic, traffic_src = pmc_traffic(n) if not c3 else (None, None)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -172,7 +181,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (numpy PCG64 seed 0x4E50; C2 layout of SURVEY.md 8d)",
-            "config": {"workload": "C2: 1M x 64-B Ethernet/IPv4/TCP records per GPU, device-resident",
+            "config": {"workload": ("C3: 8M records, frames U[64,1500] B, IPv4 TCP|UDP per GPU, device-resident"
+                                    if c3 else "C2: 1M x 64-B Ethernet/IPv4/TCP records per GPU, device-resident"),
                        "records_per_gpu": n, "capture_bytes": len(blob), "parallelism": f"record-range x{world}",
                        "outputs": "convert_records flow table (32 B/flow incl. record offset)"},
             "stream_GBps": round(stream_bytes * world * args.steps / wall / 1e9, 2),
@@ -182,7 +192,7 @@ def main():
                          "read_only_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                          "bytes_per_launch": alg, "kernel_ms": round(kern_ms, 5)},
         }
-        if not args.no_cpu:
+        if not args.no_cpu and not c3:
             out["cpu_baseline"] = cpu_baseline(blob, n, args.cpu_budget)
         print(json.dumps(out), flush=True)
     if world > 1:

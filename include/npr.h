@@ -244,7 +244,9 @@ npr_status npr_parse_extract(npr_ctx *ctx, const uint8_t *input, size_t len,
  * file, 0 for bare records), decodes every record and writes the outputs described in
  * npr_dev_outputs.  `input` is a 16-byte-aligned device pointer; `stream` a hipStream_t
  * (NULL = the context's stream).  Asynchronous: read `summary` after the stream syncs,
- * or call npr_dev_check() which also reports NPR_ERR_CAPACITY / NPR_ERR_TIMEOUT. */
+ * or call npr_dev_check() which also reports NPR_ERR_CAPACITY / NPR_ERR_TIMEOUT.
+ * A flows-only parse of a capture larger than one resident launch holds (about 80 MB on MI355X)
+ * runs as npr_dev_parse_extract_chunked. */
 npr_status npr_dev_parse_extract(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness endianness, const npr_dev_outputs *out,
                                  void *stream);
@@ -259,6 +261,22 @@ npr_status npr_dev_parse_extract(npr_ctx *ctx, const void *input, uint64_t len, 
 npr_status npr_dev_parse_extract_range(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness endianness, int speculative_start,
                                        uint64_t ref_record, const npr_dev_outputs *out, void *stream);
+/* Chained form (the resident single pass; flows-only outputs): continue the record chain, the
+ * record count and the flow rows where the launch that wrote `prev` left them (`prev` a device
+ * npr_summary of an earlier launch on this context; NULL = `start` is an exact record start).
+ * Records that START in [start, stop) are produced; their Ok flows go to the convert_records rows
+ * after prev's; *out->summary is cumulative.  A capture split at any byte boundaries and parsed
+ * chunk after chunk this way equals one npr_dev_parse_extract of the whole. */
+npr_status npr_dev_parse_extract_chain(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
+                                       uint64_t stop, npr_endianness endianness, const npr_summary *prev,
+                                       uint64_t ref_record, const npr_dev_outputs *out, void *stream);
+/* npr_dev_parse_extract in chunks of about `chunk_bytes` (0: what one launch keeps in registers,
+ * about 80 MB on MI355X), chained on the device with no host synchronisation: captures of any size
+ * at the single-launch rate.  Launches that need a record table / offsets / status run the
+ * two-pass kernels in one launch instead. */
+npr_status npr_dev_parse_extract_chunked(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
+                                         npr_endianness endianness, const npr_dev_outputs *out,
+                                         uint64_t chunk_bytes, void *stream);
 /* Synchronise `stream`, copy the summary back and map its flags to a status. */
 npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
                          npr_summary *host_summary);

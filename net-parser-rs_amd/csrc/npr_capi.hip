@@ -38,6 +38,10 @@ struct npr_ctx {
   int resident = 1;        // NPR_OPT_RESIDENT
   uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
   uint64_t res_launches = 0;  // resident launches so far (selects the arrival-counter bank)
+  DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
+  const npr_summary *sum_ptr[2] = {nullptr, nullptr};  // summaries the last two launches wrote
+  uint32_t sum_epoch[2] = {0, 0};
+  uint32_t sum_next = 0;
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
   std::string err;
@@ -98,6 +102,16 @@ inline uint16_t rd_u16(const uint8_t *p, bool big) {
   uint16_t v;
   memcpy(&v, p, 2);
   return big ? (uint16_t)__builtin_bswap16(v) : v;
+}
+
+// persistent waves of the resident single pass: CUs x resident waves per CU, at most kResMaxWaves
+npr_status res_geometry(npr_ctx *c) {
+  if (c->res_waves) return NPR_OK;
+  int cus = 0;
+  HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
+  const int per = npr::resident_waves_per_cu();
+  c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
+  return NPR_OK;
 }
 
 uint64_t tiles_for(uint64_t len, uint64_t start, uint64_t *org_out) {
@@ -161,7 +175,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
+  for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->chain, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->scratch})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
@@ -264,12 +278,60 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 // ---- device-resident hot path -----------------------------------------------------------------
 npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness e, const npr_dev_outputs *o, void *stream) {
+  // flows-only captures larger than one launch keeps in registers: chained chunks of that size
+  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start) {
+    npr_status st = res_geometry(c);
+    if (st) return st;
+    if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
+      return npr_dev_parse_extract_chunked(c, input, len, start, e, o, 0, stream);
+  }
   return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
 }
+
+static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                               npr_endianness e, int speculative_start, uint64_t ref_record,
+                               const npr_summary *prev, const npr_dev_outputs *o, void *stream);
 
 npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness e, int speculative_start,
                                        uint64_t ref_record, const npr_dev_outputs *o, void *stream) {
+  return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream);
+}
+
+npr_status npr_dev_parse_extract_chain(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
+                                       uint64_t stop, npr_endianness e, const npr_summary *prev,
+                                       uint64_t ref_record, const npr_dev_outputs *o, void *stream) {
+  return launch_range(c, input, len, start, stop, e, 0, ref_record, prev, o, stream);
+}
+
+npr_status npr_dev_parse_extract_chunked(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
+                                         npr_endianness e, const npr_dev_outputs *o, uint64_t chunk_bytes,
+                                         void *stream) {
+  if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (start > len) return fail(c, NPR_ERR_ARG, "need start <= len");
+  const bool flows_only = !o->record_offsets && !o->records && !o->record_status;
+  if (!c->resident || !flows_only)  // the two-pass kernels take any size in one launch
+    return launch_range(c, input, len, start, len, e, 0, start, nullptr, o, stream);
+  npr_status st = res_geometry(c);
+  if (st) return st;
+  uint64_t chunk = chunk_bytes ? chunk_bytes : (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
+  if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
+  npr_dev_outputs oc = *o;
+  const npr_summary *prev = nullptr;
+  uint64_t lo = start;
+  for (uint64_t k = 0;; ++k) {
+    const uint64_t hi = len - lo <= chunk ? len : lo + chunk;
+    oc.summary = hi == len ? o->summary : (npr_summary *)c->chain.p + (k & 1u);
+    if ((st = launch_range(c, input, len, lo, hi, e, 0, start, prev, &oc, stream))) return st;
+    if (hi == len) return NPR_OK;
+    prev = oc.summary;
+    lo = hi;
+  }
+}
+
+static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                               npr_endianness e, int speculative_start, uint64_t ref_record,
+                               const npr_summary *prev, const npr_dev_outputs *o, void *stream) {
   if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
   if (stop > len || start > stop) return fail(c, NPR_ERR_ARG, "need start <= stop <= len");
   if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
@@ -334,13 +396,17 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
   }
   // flows-only launches: the resident single pass, one wave per (CU x resident waves), at most
   // kResMaxWaves and at most one per tile
-  if (c->resident && !p.rec_off && !p.recs && !p.rec_status) {
-    if (!c->res_waves) {
-      int cus = 0;
-      HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
-      const int per = npr::resident_waves_per_cu();
-      c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
-    }
+  const bool resident = c->resident && !p.rec_off && !p.recs && !p.rec_status;
+  if (prev) {
+    if (!resident) return fail(c, NPR_ERR_ARG, "a chained launch produces flows only (resident pass)");
+    if (speculative_start) return fail(c, NPR_ERR_ARG, "a chained launch continues an exact chain");
+    p.prev = prev;
+    p.prev_epoch = 0;  // the epoch of the launch that wrote *prev, when it was one of ours
+    for (int i = 0; i < 2; ++i)
+      if (c->sum_ptr[i] == prev) p.prev_epoch = c->sum_epoch[i];
+  }
+  if (resident) {
+    if ((st = res_geometry(c))) return st;
     uint64_t wv = std::min<uint64_t>(nt, c->res_waves);
     if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
     p.nwaves = (uint32_t)wv;
@@ -352,6 +418,9 @@ npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t l
     p.rready = (uint64_t *)((char *)c->abort_word + kCtlFlags);
   }
   HIP_CHECK(c, npr::launch_parse_extract(p, s));
+  c->sum_ptr[c->sum_next] = o->summary;  // who wrote which summary (chained launches check it)
+  c->sum_epoch[c->sum_next] = c->epoch;
+  c->sum_next ^= 1u;
   return NPR_OK;
 }
 

@@ -54,6 +54,10 @@ struct alignas(128) RangeSlot {
 };
 static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
 constexpr uint32_t kResMaxWaves = 64 * 64;  // at most 4096 persistent waves
+#ifndef NPR_RES_SLOTS
+#define NPR_RES_SLOTS 6
+#endif
+constexpr int kResSlots = NPR_RES_SLOTS;    // 64-record rounds of flows held in registers per wave
 constexpr uint32_t kResWgMin = 16;          // waves per workgroup (npr_kernels.hip kResWg) is at least this
 
 // exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
@@ -110,6 +114,8 @@ struct ParseParams {
   uint32_t *rcnt;          // arrival counters (zero at launch): group g at [16 g], the group folds at [16 * 64]
   uint32_t *rcnt_next;     // the other bank: zeroed by this launch for the next resident launch
   uint64_t *rready;        // per-workgroup ready granule (8 words apart): every G(b) published
+  const npr_summary *prev; // chained launch (resident pass only): continue the chain and the counts
+  uint32_t prev_epoch;     //   of the launch that wrote *prev (its epoch, 0 = unchecked); NULL = none
 };
 
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)

@@ -362,7 +362,9 @@ __device__ __forceinline__ uint64_t rl64(uint64_t v, int lane) {
 
 // a value every lane holds identically, made visibly wave-uniform (scalar registers)
 __device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  return ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)v);
+  // (readfirstlane returns int: widen through uint32_t, or offsets past 2 GiB sign-extend)
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
 }
 
 // A segment of consecutive tiles [first, last] under speculation: the chain entered at `entry`
@@ -1302,13 +1304,9 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
 //     from the exact position.  A contradiction below v waits for the offending wave's exact
 //     prefix P(m), published at the end of its own phase B.
 // =============================================================================================
-#ifndef NPR_RES_SLOTS
-#define NPR_RES_SLOTS 6
-#endif
 #ifndef NPR_RES_RING
 #define NPR_RES_RING 2
 #endif
-constexpr int kResSlots = NPR_RES_SLOTS;  // 64-record rounds of flows held in registers per wave
 constexpr int kResRing = NPR_RES_RING;    // LDS tile slots per wave (1 processed + kResRing-1 in flight)
 constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
 #ifndef NPR_RES_WG
@@ -1669,7 +1667,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   uint32_t c0 = 0, c1 = 0;
   if (active) res_range(kp, v, c0, c1);
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
-  const bool spec0 = (kp.flags & kFlagSpecStart) != 0;
+  const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;  // chained: tile 0 speculates too
   if (v == 0) {  // zero the other counter bank for the next resident launch
     kp.rcnt_next[16u * lane] = 0u;
     if (lane == 0) kp.rcnt_next[16u * 64u] = 0u;
@@ -1856,7 +1854,14 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
           G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz);
         }
       }
-      if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
+      if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
+        const uint64_t pc = kp.prev->consumed, pr = kp.prev->n_records, pf = kp.prev->n_flows;
+        okw = okw && (kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch);  // it completed
+        entry0 = kp.prev->entry;  // the chain's first record, as the first link reported it
+        E.entry = E.exit = pc;
+        E.cnt = pr;
+        E.ok = pf;
+      } else if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
         entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
         E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
       }

@@ -87,7 +87,8 @@ EXPORTED = [
     "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps", "npr_ctx_set_option",
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
-    "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_check", "npr_dev_extract_flows",
+    "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
+    "npr_dev_parse_extract_chunked", "npr_dev_check", "npr_dev_extract_flows",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -122,6 +123,11 @@ _SIGNATURES = {
     "npr_dev_parse_extract_range": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                    ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                                    ctypes.POINTER(DevOutputsC), _vp]),
+    "npr_dev_parse_extract_chain": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                   ctypes.c_int, _vp, ctypes.c_uint64,
+                                                   ctypes.POINTER(DevOutputsC), _vp]),
+    "npr_dev_parse_extract_chunked": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                                     ctypes.POINTER(DevOutputsC), ctypes.c_uint64, _vp]),
     "npr_dev_check": (ctypes.c_int, [_vp, ctypes.POINTER(DevOutputsC), _vp, ctypes.POINTER(SummaryC)]),
     "npr_dev_extract_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                              _vp, _vp, _vp, _vp]),

@@ -58,6 +58,18 @@ class Workspace:
         self.ctx.check(st)
         self._stream = s
 
+    def launch_chunked(self, buf, start=24, endianness=_abi.LITTLE, chunk_bytes=0, nbytes=None, stream=None):
+        """The capture in chunks of ~chunk_bytes chained on the device (npr_dev_parse_extract_chunked):
+        one launch per chunk, no host synchronisation, same outputs as launch()."""
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        n = buf.numel() if nbytes is None else int(nbytes)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        st = self.ctx.lib.npr_dev_parse_extract_chunked(self.ctx.handle, buf.data_ptr(), n, int(start), endianness,
+                                                        ctypes.byref(self.outs), int(chunk_bytes),
+                                                        ctypes.c_void_p(s.cuda_stream))
+        self.ctx.check(st)
+        self._stream = s
+
     def check(self):
         sm = _abi.SummaryC()
         st = self.ctx.lib.npr_dev_check(self.ctx.handle, ctypes.byref(self.outs),

@@ -264,3 +264,83 @@ def test_mirror_api_matches_oracle():
     assert recs2.len() == len(recs)
     recs_list = npr.CaptureParser.parse_file(blob)
     assert len(recs_list) == len(recs)
+
+
+# ---- chained launches (npr_dev_parse_extract_chunked): the capture parsed chunk after chunk --------
+def check_chunked(blob, chunk, start=24, endianness=None):
+    if start == 24:
+        rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
+        e = hdr.endianness if endianness is None else endianness
+    else:
+        e = endianness
+        want_recs, cons = _oracle.records_parse(blob[start:], e)
+        want_recs = want_recs.copy()
+        want_recs["offset"] += start
+        want_cons = start + cons
+    want_flows, want_v6 = _oracle.convert_records(blob, want_recs)
+    cap = max((len(blob) - start) // 16 + 1, 1)
+    w = device.Workspace(cap, cap, records=False, status=False)
+    w.launch_chunked(to_dev(blob), start=start, endianness=e, chunk_bytes=chunk, nbytes=len(blob))
+    sm = w.check()
+    assert (sm.n_records, sm.n_flows, sm.consumed) == (len(want_recs), len(want_flows), want_cons)
+    assert sm.entry == start  # the chain's first record, carried through every link
+    got = w.flows_np()
+    assert got.tobytes() == want_flows.tobytes(), first_diff(got, want_flows)
+    v6mask = (want_flows["kind"] & _abi.KIND_IPV6) != 0
+    if v6mask.any():
+        assert w.flows_v6_np()[v6mask].tobytes() == want_v6[v6mask].tobytes()
+    return sm
+
+
+CHUNKS = pytest.mark.parametrize("chunk", [1000, 4096, 40_000, 333_333])
+
+
+@CHUNKS
+@pytest.mark.parametrize("corpus", ["c2", "c3", "quirk", "adversarial", "jumbo", "v6"])
+def test_chunked_matches_serial(corpus, chunk):
+    blob = {"c2": lambda: synth.fixed64(30_000),
+            "c3": lambda: synth.variable_mix(8_000),
+            "quirk": lambda: synth.quirk_corpus(6_000, seed=52),
+            "adversarial": lambda: synth.quirk_corpus(3_000, seed=53, fake_every=3, zero_every=7, jumbo_every=150),
+            "jumbo": lambda: synth.quirk_corpus(400, seed=54, jumbo_every=2),
+            "v6": lambda: synth.quirk_corpus(5_000, seed=55, big=True)}[corpus]()
+    check_chunked(blob, chunk)
+
+
+@CHUNKS
+def test_chunked_chain_end_and_tails(chunk):
+    sm = check_chunked(synth.corrupt_midfile(synth.fixed64(20_000), at_record=7_777), chunk)
+    assert sm.n_records == 7_777
+    for tail in ("truncated_header", "truncated_payload", "huge_incl"):
+        check_chunked(synth.quirk_corpus(2_000, seed=56, tail=tail), chunk)
+
+
+def test_chunked_bare_records_and_tiny_inputs():
+    body = synth.quirk_corpus(3_000, seed=57, with_header=False)
+    check_chunked(body, 5_000, start=0, endianness=npr.Endianness.Little)
+    check_chunked(synth.global_header(), 4096)
+    check_chunked(synth.global_header() + bytes(10), 7)
+
+
+def test_capture_past_2GiB():
+    """C3-shaped capture of ~2.2 GB: record offsets past 2^31 (a sign-extension regression), both
+    kernel families, against the oracle."""
+    n = 2_800_000
+    blob = synth.variable_mix(n)
+    rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
+    want_flows, _ = _oracle.convert_records(blob, want_recs)
+    buf = to_dev(blob)
+    del blob
+    ctx = npr.context(0)
+    try:
+        for resident in (1, 0):
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, resident))
+            w = device.Workspace(n + 1, n + 1, records=False, status=False)
+            w.launch(buf, start=24, endianness=hdr.endianness)
+            sm = w.check()
+            assert (sm.n_records, sm.n_flows, sm.consumed) == (len(want_recs), len(want_flows), want_cons)
+            got = w.flows_np()
+            assert got.tobytes() == want_flows.tobytes(), first_diff(got, want_flows)
+            del w
+    finally:
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
