@@ -183,11 +183,18 @@ const char *npr_ctx_last_error(const npr_ctx *ctx);
  * start; the others are reserved (0). */
 npr_status npr_ctx_set_stats(npr_ctx *ctx, int enable);
 npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
-/* With npr_ctx_set_stats(ctx, 2): per-tile s_memrealtime (100 MHz) stamps of the last parse,
- * 16 words per tile: pass 1 [0] tile start [1] entry known [2] walked [3] counted [4] published;
- * pass 2 [5] tile start [6] record offsets known [7] written; on the first tile of a wave's
- * chunk: [8] pass-2 entry [9] prologue issued [10] prefix known [11]/[12] pass-1 group arrival
- * start/end.  out may be NULL with cap 0 to query *n_tiles only. */
+/* With npr_ctx_set_stats(ctx, 2): s_memrealtime (100 MHz) stamps of the last parse, 16 words
+ * per row (the buffer holds one row per tile).
+ * Resident pass (flows-only launches): row v = persistent wave v: [0] start [1] first tile landed
+ *   [2] phase A done [3] range aggregate published + workgroup fold [4] prefix known [5] kept
+ *   flows written [6] done; [8] tiles [9] kept rounds [10] deferred tiles [11] 1 = fast path;
+ *   the first wave of each workgroup also [12] ready granule seen [13] aggregate windows landed
+ *   [14] workgroup prefix folded (scripts/res_stamps.py reads them).
+ * Two-pass kernels: row t = tile t: pass 1 [0] tile start [1] entry known [2] walked [3] counted
+ *   [4] published; pass 2 [5] tile start [6] record offsets known [7] written; on the first tile
+ *   of a wave's chunk: [8] pass-2 entry [9] prologue issued [10] prefix known [11]/[12] pass-1
+ *   group arrival start/end.
+ * out may be NULL with cap 0 to query *n_tiles only. */
 npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64_t *n_tiles);
 /* Context options.
  * NPR_OPT_RESIDENT (default 1; env NPR_RESIDENT=0 sets 0 at create): a flows-only device parse
