@@ -203,8 +203,15 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   convert_records rows are known.  0 (and every launch that asks for a record table, offsets or
  *   status) runs the two-pass kernels; N > 1 caps the resident pass at N waves (longer ranges per
  *   wave: a test knob).  Same results either way.
+ * NPR_OPT_STREAM_CHUNK (KiB, default 0 = off): npr_parse_extract without a record table
+ *   copies a capture of more than two chunks to the device in chunks on a second stream and
+ *   launches each chunk's chained parse as soon as it (and the next chunk) has landed, so the
+ *   H2D copy overlaps the parse.  Results are those of the unchunked parse: a record longer than
+ *   a chunk ends a link early, which the call detects and answers by parsing the staged capture
+ *   again in one go.  Off by default: from pageable host memory the chunked copies measured
+ *   slower than one copy, and the copy is ~50x the parse, so overlap gains little.
  * NPR_OPT_PARK_FLOWS: accepted for ABI 2 callers, no effect. */
-enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2 };
+enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <string>
+#include <vector>
 
 #include "../../include/npr.h"
 #include "npr_internal.hpp"
@@ -44,6 +45,11 @@ struct npr_ctx {
   uint32_t sum_next = 0;
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
+  // host flows-only parses: the capture's H2D copy in chunks on copy_stream, each chunk's chained
+  // launch as soon as its bytes (and the next chunk's, for records that straddle) have landed
+  uint64_t stream_chunk = 0;  // NPR_OPT_STREAM_CHUNK (KiB in the option; 0 = one copy, the default)
+  hipStream_t copy_stream = nullptr;
+  std::vector<hipEvent_t> copied;       // one per chunk in flight
   std::string err;
 };
 
@@ -182,6 +188,9 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (c->summary) (void)hipFree(c->summary);
   if (c->summary_h) (void)hipHostFree(c->summary_h);
   if (c->stats) (void)hipFree(c->stats);
+  if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  for (hipEvent_t ev : c->copied) (void)hipEventDestroy(ev);
+  if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -197,6 +206,10 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
     case NPR_OPT_RESIDENT:  // 0 off, 1 auto, N > 1: at most N waves (tests: long ranges, deferral)
       if (value < 0) return fail(c, NPR_ERR_ARG, "NPR_OPT_RESIDENT must be >= 0");
       c->resident = value;
+      return NPR_OK;
+    case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first
+      if (value < 0 || (value > 0 && value < 64)) return fail(c, NPR_ERR_ARG, "NPR_OPT_STREAM_CHUNK: 0 or >= 64 KiB");
+      c->stream_chunk = (uint64_t)value << 10;
       return NPR_OK;
     default:
       return fail(c, NPR_ERR_ARG, "unknown option");
@@ -455,12 +468,60 @@ static npr_status stage_input(npr_ctx *c, const uint8_t *in, size_t len) {
   return NPR_OK;
 }
 
+// Flows-only host parse, overlapped: chunk j = bytes [a_j, a_j+1) of the capture (a_j = j x chunk)
+// goes H2D on copy_stream; link j of the chain (records starting in [max(start, a_j), a_j+1))
+// launches on the compute stream once chunks j and j+1 have landed, reading at most up to a_j+2.
+// A record longer than a chunk therefore ends that link's chain early; the caller checks for
+// that on the host and parses again without streaming (npr_dev_parse_extract_chain semantics
+// otherwise: same rows, counts and summary as one launch).
+static npr_status stream_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64_t start, npr_endianness e,
+                               const npr_dev_outputs *o) {
+  const uint64_t chunk = c->stream_chunk;
+  const uint64_t nchunks = (len + chunk - 1) / chunk;
+  npr_status st = ensure(c, c->in, len + 16);
+  if (st) return st;
+  if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
+  if (!c->copy_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  while (c->copied.size() < nchunks) {
+    hipEvent_t ev;
+    HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    c->copied.push_back(ev);
+  }
+  uint8_t *dev = (uint8_t *)c->in.p;
+  // the compute stream's earlier work (a previous parse reading the staging buffer) comes first
+  HIP_CHECK(c, hipEventRecord(c->copied[0], c->stream));
+  HIP_CHECK(c, hipStreamWaitEvent(c->copy_stream, c->copied[0], 0));
+  for (uint64_t j = 0; j < nchunks; ++j) {
+    const uint64_t a = j * chunk, b = std::min<uint64_t>(len, a + chunk);
+    HIP_CHECK(c, hipMemcpyAsync(dev + a, in + a, b - a, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_CHECK(c, hipEventRecord(c->copied[j], c->copy_stream));
+  }
+  npr_dev_outputs oc = *o;
+  const npr_summary *prev = nullptr;
+  uint64_t k = 0;
+  for (uint64_t j = 0; j < nchunks; ++j) {
+    const uint64_t lo = std::max<uint64_t>(start, j * chunk), hi = std::min<uint64_t>(len, (j + 1) * chunk);
+    if (hi <= lo && hi < len) continue;  // (start past this chunk)
+    const uint64_t jn = std::min<uint64_t>(j + 1, nchunks - 1);
+    HIP_CHECK(c, hipStreamWaitEvent(c->stream, c->copied[jn], 0));
+    const uint64_t readable = std::min<uint64_t>(len, (jn + 1) * chunk);
+    oc.summary = hi == len ? o->summary : (npr_summary *)c->chain.p + (k++ & 1u);
+    if ((st = launch_range(c, dev, readable, lo, hi, e, 0, start, prev, &oc, c->stream))) return st;
+    if (hi == len) break;
+    prev = oc.summary;
+  }
+  return NPR_OK;
+}
+
 // Shared body of records_parse / capture_file_parse / parse_extract.
 static npr_status host_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64_t start, npr_endianness e,
                              npr_record *out_recs, size_t rec_cap, size_t *n_records, npr_flow *out_flows,
                              npr_flow_v6 *out_v6, size_t flow_cap, size_t *n_flows, size_t *consumed) {
   HIP_CHECK(c, hipSetDevice(c->device));
-  npr_status st = stage_input(c, in, len);
+  // flows only, a capture of several chunks: copies overlapped with the parse
+  const bool streamed = !out_recs && c->resident && c->stream_chunk && len > start &&
+                        len - start > 2 * c->stream_chunk && len > start + 16;
+  npr_status st = streamed ? NPR_OK : stage_input(c, in, len);
   if (st) return st;
   const uint64_t max_rec = len > start ? (len - start) / 16 + 1 : 1;
   const uint64_t rcap = std::min<uint64_t>(rec_cap, max_rec);
@@ -481,10 +542,19 @@ static npr_status host_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64_t
     }
   }
   o.summary = c->summary;
-  if ((st = npr_dev_parse_extract(c, c->in.p, len, start, e, &o, c->stream))) return st;
+  if ((st = streamed ? stream_parse(c, in, len, start, e, &o) : npr_dev_parse_extract(c, c->in.p, len, start, e, &o, c->stream)))
+    return st;
   npr_summary sm;
   st = npr_dev_check(c, &o, c->stream, &sm);
   if (st && st != NPR_ERR_CAPACITY) return st;
+  if (streamed && sm.consumed + 16 <= len) {  // the chain stopped at a complete record: one longer
+    const uint64_t incl = rd_u32(in + sm.consumed + 8, e == NPR_BIG);  // than a chunk; parse again whole
+    if (incl <= len - sm.consumed - 16) {
+      if ((st = npr_dev_parse_extract(c, c->in.p, len, start, e, &o, c->stream))) return st;
+      st = npr_dev_check(c, &o, c->stream, &sm);
+      if (st && st != NPR_ERR_CAPACITY) return st;
+    }
+  }
   const uint64_t nr = std::min<uint64_t>(sm.n_records, rcap);
   const uint64_t nf = std::min<uint64_t>(sm.n_flows, fcap);
   if (o.records && nr)

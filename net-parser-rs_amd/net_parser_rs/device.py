@@ -128,3 +128,23 @@ def parse_extract(buf, start=24, endianness=_abi.LITTLE, record_cap=None, flow_c
     ws.launch(buf, start=start, endianness=endianness)
     sm = ws.check()
     return Result(ws, sm)
+
+
+def host_parse_extract(data, flow_cap=None, with_v6=True, ctx=None):
+    """npr_parse_extract without a record table: a host capture (bytes / uint8 array) in, the
+    convert_records flow table out on the host.  Captures of more than two NPR_OPT_STREAM_CHUNK
+    chunks are copied in chunks overlapped with the chained parse.  Returns (flows, flows_v6 or
+    None, n_flows, consumed, header)."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    ctx = ctx or context(0)
+    cap = max((a.size - 24) // 16 + 1, 1) if flow_cap is None else flow_cap
+    flows = np.zeros(cap, dtype=_abi.FLOW_DTYPE)
+    v6 = np.zeros(cap, dtype=_abi.FLOW_V6_DTYPE) if with_v6 else None
+    hdr = _abi.GlobalHeaderC()
+    n_flows, consumed = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    st = ctx.lib.npr_parse_extract(ctx.handle, a.ctypes.data if a.size else None, a.size, ctypes.byref(hdr), None, 0,
+                                   None, flows.ctypes.data, v6.ctypes.data if v6 is not None else None, cap,
+                                   ctypes.byref(n_flows), ctypes.byref(consumed))
+    ctx.check(st)
+    k = min(n_flows.value, cap)
+    return flows[:k], (v6[:k] if v6 is not None else None), n_flows.value, consumed.value, hdr
