@@ -1833,6 +1833,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     // (2) every G published (this workgroup's ready granule: a returning-atomic poll, one poller per
     //     granule), then E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1): all windows in one round trip
     bool okw = res_sentinel(kp, kp.rready + 8u * b, t0);
+    if (DIAG) stamp_at(st, 12);
     Seg E = start_seg(kp);
     uint64_t entry0 = kp.start;
     if (okw) {
@@ -1854,6 +1855,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
           G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz);
         }
       }
+      if (DIAG) stamp_at(st, 13);
       if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
         const uint64_t pc = kp.prev->consumed, pr = kp.prev->n_records, pf = kp.prev->n_flows;
         okw = okw && (kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch);  // it completed
@@ -1872,6 +1874,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
       }
     }
+    if (DIAG) stamp_at(st, 14);
     // (3) each wave's prefix
     if ((uint32_t)lane < nw) sh.x[lane] = lane == 0 ? E : combine(kp, E, e);
     if (lane == 0) {
@@ -1945,7 +1948,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     st.v[9] = ns;
     st.v[10] = c1 - tdef;
     st.v[11] = (entry != kNone && xe == pos) ? 1 : 0;
-    stamp_flush(kp, st, v, 0xF7Fu);
+    stamp_flush(kp, st, v, wid == 0 ? 0x7F7Fu : 0xF7Fu);
   }
 }
 
