@@ -188,7 +188,7 @@ npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
  * Resident pass (flows-only launches): row v = persistent wave v: [0] start [1] first tile landed
  *   [2] phase A done [3] range aggregate published + workgroup fold [4] prefix known [5] kept
  *   flows written [6] done; [8] tiles [9] kept rounds [10] deferred tiles [11] 1 = fast path;
- *   the first wave of each workgroup also [12] ready granule seen [13] aggregate windows landed
+ *   the first wave of each workgroup also [12] look-back start [13] lower aggregates all landed
  *   [14] workgroup prefix folded (scripts/res_stamps.py reads them).
  * Two-pass kernels: row t = tile t: pass 1 [0] tile start [1] entry known [2] walked [3] counted
  *   [4] published; pass 2 [5] tile start [6] record offsets known [7] written; on the first tile

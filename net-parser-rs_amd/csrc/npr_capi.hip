@@ -55,10 +55,8 @@ struct npr_ctx {
 
 namespace {
 
-// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each),
-// per-workgroup ready granules (64 B apart)
-constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlFlags = kCtlCounters + 2 * kCtlBank,
-                 kCtlBytes = kCtlFlags + (npr::kResMaxWaves / npr::kResWgMin) * 64;
+// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each)
+constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlBytes = kCtlCounters + 2 * kCtlBank;
 constexpr uint32_t kTimeoutTicks = 100u * 1000u * 1000u;  // 1 s of s_memrealtime (100 MHz)
 
 npr_status fail(npr_ctx *c, npr_status st, const char *fmt, ...) {
@@ -428,7 +426,6 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     const uint64_t bank = c->res_launches++ & 1u;  // this launch counts in a bank the previous one zeroed
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters + bank * kCtlBank);
     p.rcnt_next = (uint32_t *)((char *)c->abort_word + kCtlCounters + (bank ^ 1u) * kCtlBank);
-    p.rready = (uint64_t *)((char *)c->abort_word + kCtlFlags);
   }
   HIP_CHECK(c, npr::launch_parse_extract(p, s));
   c->sum_ptr[c->sum_next] = o->summary;  // who wrote which summary (chained launches check it)

@@ -113,7 +113,6 @@ struct ParseParams {
   GroupSlot *rgroups;      // [ceil(nwaves / 64)]
   uint32_t *rcnt;          // arrival counters (zero at launch): group g at [16 g], the group folds at [16 * 64]
   uint32_t *rcnt_next;     // the other bank: zeroed by this launch for the next resident launch
-  uint64_t *rready;        // per-workgroup ready granule (8 words apart): every G(b) published
   const npr_summary *prev; // chained launch (resident pass only): continue the chain and the counts
   uint32_t prev_epoch;     //   of the launch that wrote *prev (its epoch, 0 = unchecked); NULL = none
 };

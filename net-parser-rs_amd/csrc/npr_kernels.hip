@@ -1820,19 +1820,16 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     Seg e, agg;
     res_fold_lanes(kp, L, (int)nw, e, agg);
     // G(b), then the arrival.  No store drain in between: readers check the granules' tags and
-    // re-read (returning atomics) until they are this launch's
+    // re-read (returning atomics) until they are this launch's.  Nothing waits for the count: the
+    // arrival's round trip only paces the first window read below (measured 0.3 us better than
+    // reading at once, which re-reads more aggregates that are not published yet)
     if (lane == 0) put_agg(kp, kp.rgroups + b, agg);
-    uint32_t last = 0;
-    if (lane == 0) last = res_arrive(kp.rcnt + 16u * 64u) == nb;
-    if (__builtin_amdgcn_readfirstlane(last)) {  // the last arrival tells every workgroup, one granule each
-#pragma unroll
-      for (uint32_t k = 0; k < kResMaxWaves / kResWgMin; k += 64)
-        if (k + lane < nb) st_agent(kp.rready + 8u * (k + lane), gran(ep, 1));
-    }
+    if (lane == 0) (void)res_arrive(kp.rcnt + 16u * 64u);
     if (DIAG) stamp_at(st, 3);
-    // (2) every G published (this workgroup's ready granule: a returning-atomic poll, one poller per
-    //     granule), then E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1): all windows in one round trip
-    bool okw = res_sentinel(kp, kp.rready + 8u * b, t0);
+    // (2) E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1), looking back: every window read at once, then
+    //     only the aggregates that are not this launch's yet re-read, until all are (a workgroup
+    //     proceeds as soon as the ones below it are published, not when the whole grid is)
+    bool okw = true;
     if (DIAG) stamp_at(st, 12);
     Seg E = start_seg(kp);
     uint64_t entry0 = kp.start;
@@ -1843,16 +1840,29 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
         G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
       }
+      // every window at once: re-read (returning atomics) only the aggregates not yet this
+      // launch's -- not published yet, or a line an earlier launch left in this XCD's L2
+      uint32_t nap = 1;
+      for (int tries = 0;; ++tries) {
+        bool miss = false;
 #pragma unroll
-      for (int w = 0; w < kTopWin; ++w) {  // not landed yet, or a line an earlier launch left in this XCD's L2
-        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-        uint32_t nap = 1;
-        for (int tries = 0; __ballot((uint32_t)lane < sz && !G[w].present); ++tries) {
-          if (tries && !res_nap(kp, t0, nap)) {
-            okw = false;
-            break;
+        for (int w = 0; w < kTopWin; ++w) {
+          const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+          miss = miss || __ballot((uint32_t)lane < sz && !G[w].present) != 0ull;
+        }
+        if (!miss) break;
+        if (tries && !res_nap(kp, t0, nap)) {
+          okw = false;
+          break;
+        }
+#pragma unroll
+        for (int w = 0; w < kTopWin; ++w) {
+          const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+          const bool need = (uint32_t)lane < sz && !G[w].present;
+          if (__ballot(need)) {
+            const LaneSeg N = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, need);
+            if (need) G[w] = N;
           }
-          G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz);
         }
       }
       if (DIAG) stamp_at(st, 13);

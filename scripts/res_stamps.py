@@ -23,5 +23,5 @@ if len(w0):
     A = S(2)
     amax = np.array([A[i:i + 16].max() for i in w0])
     print("workgroup wave 0 (last A in the workgroup = 0):")
-    for k, nm in [(3, "arrived"), (12, "ready seen"), (13, "G landed"), (14, "E folded"), (4, "prefix")]:
+    for k, nm in [(3, "arrived"), (12, "lookback"), (13, "G landed"), (14, "E folded"), (4, "prefix")]:
         print(f"  {nm:10s} {pc(S(k)[w0] - amax.max())}   (rel. to the last A of the launch)")
