@@ -1,14 +1,20 @@
 """bench.py — device-resident record parse + extract_flow (+ convert_records) on MI355X.
 
-One "step" = one launch of the resident single-pass HIP kernel (k_parse_resident) over one capture
-already resident in HBM: CaptureFile::parse (record chain) + extract_flow for every record +
-convert_records (Ok flows, reverse order), i.e. the reference's `extract` bench
-(benches/benches.rs:40-74).
+One "step" = one pass of the hot path over one capture already resident in HBM: CaptureFile::parse
+(record chain) + extract_flow for every record + convert_records (Ok flows, reverse order), i.e.
+the reference's `extract` bench (benches/benches.rs:40-74).
 
-Workload (BASELINE.json configs[1], "C2"): 1,000,000 synthetic 64-B Ethernet/IPv4/TCP records per
-GPU (80,000,024 B capture).  N > 1: one process per GPU, each parses its own 1M-record shard
-(weak scaling, no collective in the timed region).  Steps rotate over 4 copies of the capture
-(4 x 80 MB > the 256 MiB Infinity Cache together with the outputs) so every step reads HBM.
+Workloads (BASELINE.json configs; SURVEY.md §8 d):
+  c2  (default at N=1, the headline) 1,000,000 synthetic 64-B Ethernet/IPv4/TCP records
+      (80,000,024 B), one k_parse_resident launch per step; steps rotate over 4 copies of the
+      capture (4 x 80 MB > the 256 MiB Infinity Cache with the outputs), so every step reads HBM.
+  c3  8,000,000 records, frames U[64,1500] B, IPv4 TCP|UDP (6.4 GB): chained resident launches.
+  c4  (default at N>1) the 64M x 64-B capture sharded by record range, 8M records per GPU (weak
+      scaling: N=8 is exactly configs[3]).  Each rank holds ONLY its shard's file bytes; a step is
+      its shard's parse (npr_dev_parse_extract_shard) + the one exchange (an RCCL all-gather of the
+      device summaries, then the host replay of the serial chain).  The flow-table gather to rank 0
+      over RCCL (point-to-point into the merged table) is timed separately: `gather_ms`,
+      `end_to_end_Mpps`.
 
 Prints ONE JSON line on rank 0.
 """
@@ -27,36 +33,59 @@ sys.path.insert(0, os.path.join(REPO, "net-parser-rs_amd"))
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 import net_parser_rs as npr  # noqa: E402
-from net_parser_rs import device, synth  # noqa: E402
+from net_parser_rs import device, parallel, synth  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "Mpackets/s + GB/s, device-resident record parse+extract_flow, 1M×64B batch"
+C4_PER_GPU = 8_000_000
 
 
-def cpu_baseline(blob, n_records, budget_s):
-    """The CPU oracle (C restatement of the reference path, tests/_oracle.py) on 1 core."""
+def host_threads():
+    """The host cores this process may use (the GPU box gives one GPU's job 16)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, env if env > 0 else n, 16))
+
+
+def cpu_baseline(blob, n_records, budget_s, sample):
+    """The CPU oracle (C restatement of the reference path, tests/_oracle.py), CaptureFile::parse +
+    convert_records on the same capture: on all host threads (the reported baseline) and on one
+    core (the reference itself is single-threaded, benches/benches.rs)."""
     import _oracle
     rec = np.zeros(n_records + 1, dtype=npr._abi.RECORD_DTYPE)
     fl = np.zeros(n_records + 1, dtype=npr._abi.FLOW_DTYPE)
     v6 = np.zeros(n_records + 1, dtype=npr._abi.FLOW_V6_DTYPE)
-    _oracle.bench_extract(blob, rec, fl, v6)  # warm
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        k, nr = _oracle.bench_extract(blob, rec, fl, v6)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
-    assert nr == n_records
-    rate = passes * n_records / el / 1e6
-    return {"value": round(rate, 3), "unit": "Mpackets/s", "cores": 1, "kind": "port",
-            "sample": f"C2 capture ({n_records} records, {len(blob)} B) x {passes} passes, "
-                      f"CaptureFile::parse + convert_records, {el:.1f} s on 1 host core"}
+
+    def timed(fn):
+        fn()  # warm (first touch of the scratch)
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            k, nr = fn()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s:
+                break
+        assert nr == n_records
+        return passes * n_records / el / 1e6, passes, el
+
+    one, p1, e1 = timed(lambda: _oracle.bench_extract(blob, rec, fl, v6))
+    del fl, v6
+    T = host_threads()
+    mt = _oracle.MtScratch(n_records + 1)
+    many, pm, em = timed(lambda: _oracle.bench_extract_mt(blob, mt, T))
+    return {"value": round(many, 3), "unit": "Mpackets/s", "cores": T, "kind": "port",
+            "single_core_value": round(one, 3),
+            "sample": f"{sample} ({n_records} records, {len(blob)} B): CaptureFile::parse + convert_records "
+                      f"(oracle/npr_oracle.c), {pm} passes in {em:.1f} s on {T} host threads (serial chain walk, "
+                      f"parallel extract_flow); {p1} passes in {e1:.1f} s on 1 core"}
 
 
 def pmc_traffic(records):
     """HBM-side bytes per launch from the newest committed PMC summary of this workload (profiles/),
-    or None.  Collected by scripts/pmc.sh: FETCH_SIZE x2 + WRITE_SIZE summed over both kernels."""
+    or None.  Collected by scripts/pmc.sh: FETCH_SIZE x2 + WRITE_SIZE."""
     import glob
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
         try:
@@ -68,58 +97,49 @@ def pmc_traffic(records):
     return None, None
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", choices=["c2", "c3"], default="c2",
-                    help="c2 (the headline: 1M x 64-B records) or c3 (8M records, frames U[64,1500], ~6.4 GB; "
-                         "parsed as chained ~80 MB launches)")
-    ap.add_argument("--records", type=int, default=None)
-    ap.add_argument("--copies", type=int, default=None)
-    ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
-    args = ap.parse_args()
+def roofline(read_b, write_b, kern_ms, traffic=None, traffic_src=None, stream_b=None):
+    alg = read_b + write_b
+    achieved = alg / (kern_ms * 1e-3) / 1e9
+    r = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+         "read_only_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+         "bytes_per_launch": alg, "kernel_ms": round(kern_ms, 5)}
+    if stream_b is not None:
+        r["stream_GBps"] = round(stream_b / (kern_ms * 1e-3) / 1e9, 1)
+    return r
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
 
+def run_single(args, dev, local):
+    """c2 / c3 (and c4 at N=1): one GPU, the whole capture in its HBM."""
     c3 = args.config == "c3"
-    n = args.records or (8_000_000 if c3 else 1_000_000)
-    copies = args.copies or (1 if c3 else 4)
-    # same capture on every rank: each GPU parses its own shard
-    blob = synth.variable_mix(n) if c3 else synth.fixed64(n)
+    c4 = args.config == "c4"
+    n = args.records or (8_000_000 if c3 else (C4_PER_GPU if c4 else 1_000_000))
+    copies = args.copies or (4 if args.config == "c2" else 1)
+    if c4:
+        blob = synth.fixed64_range(0, n).tobytes()
+    else:
+        blob = synth.variable_mix(n) if c3 else synth.fixed64(n)
     host = torch.frombuffer(bytearray(blob), dtype=torch.uint8)
     bufs = [host.to(dev) for _ in range(copies)]
+    del host
     hdr = npr.GlobalHeader.parse(blob[:24])[1]
     ws = device.Workspace(record_cap=n, flow_cap=n, device=local, records=False, offsets=False, status=False,
                           flows=True, flows_v6=True)
     stream = torch.cuda.Stream(dev)  # an explicit stream: events bracket exactly our launches
     torch.cuda.set_stream(stream)
 
-    # correctness gate for the measured configuration
+    # correctness gate for the measured configuration (tests/test_gpu_scale.py compares it bit for bit)
     ws.launch(bufs[0], start=24, endianness=hdr.endianness)
     sm = ws.check()
-    # C2: every record is an Ok flow; C3: short TCP frames with a long data offset are not (Q9)
+    # C2/C4: every record is an Ok flow; C3: short TCP frames with a long data offset are not (Q9)
     assert sm.n_records == n and sm.consumed == len(blob) and (sm.n_flows == n or c3), (sm.n_records, sm.n_flows)
     n_flows = int(sm.n_flows)
-
     for i in range(args.warmup):
         ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
     torch.cuda.synchronize()
 
-    # ONE event pair brackets the K launches on their stream (per-step events would add marker
-    # packets between launches: ~8 us of GPU time per step, scripts/launch_probe.py)
+    # ONE event pair brackets the K steps on their stream (per-step events add marker packets)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
@@ -127,73 +147,182 @@ def main():
         ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     wall = time.perf_counter() - t0
     sm = ws.check()
     assert sm.n_records == n and sm.n_flows == n_flows
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # average launch (scan + emit) on the device
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if args.stats:
-        import ctypes
-        lib, h = ws.ctx.lib, ws.ctx.handle
-        ws.ctx.check(lib.npr_ctx_set_stats(h, 2))
-        for i in range(3):
-            ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
-        ws.check()
-        st = (ctypes.c_uint32 * 8)()
-        ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
-        ntl = ctypes.c_uint64(0)
-        ws.ctx.check(lib.npr_ctx_read_stamps(h, None, 0, ctypes.byref(ntl)))  # tile count of the last launch
-        nt = ntl.value
-        stamps = np.zeros(nt * 16, dtype=np.uint64)
-        ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
-        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-        np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 16))
-        print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} tiles={nt}", file=sys.stderr, flush=True)
-        ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
+        stats_dump(ws, bufs, hdr, copies, 0)
+    read_b = len(blob)   # every byte of the capture is read (C2: = SURVEY 8d's 16 + min(incl, 64) per record)
+    write_b = 32 * n_flows
+    traffic, src = pmc_traffic(n) if args.config == "c2" else (None, None)
+    out = base_line(args, 1, wall, n, len(blob))
+    out["config"].update({"records_per_gpu": n, "capture_bytes": len(blob), "parallelism": "single GPU"})
+    out["roofline"] = roofline(read_b, write_b, kern_ms, traffic, src, stream_b=len(blob) - 24)
+    if c3:
+        sd = 16 * n + 64 * n  # SURVEY 8d bytes of C3: 16 + min(incl, 64) read per record (+ 32 written)
+        out["roofline"]["survey_8d_bytes_per_launch"] = sd + write_b
+        out["roofline"]["survey_8d_frac"] = round((sd + write_b) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        out["roofline"]["note"] = ("C3 records are ~800 B: record boundaries are unknown until the chain is walked, "
+                                   "so the whole capture streams (achieved/frac use the stream bytes)")
+    if not args.no_cpu:
+        sample = {"c2": "the C2 capture", "c3": "the C3 capture", "c4": "one C4 shard"}[args.config]
+        out["cpu_baseline"] = cpu_baseline(blob, n, args.cpu_budget, sample)
+    return out
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall, kern_ms = float(t[0]), float(t[1])
 
+def stats_dump(ws, bufs, hdr, copies, rank):
+    import ctypes
+    lib, h = ws.ctx.lib, ws.ctx.handle
+    ws.ctx.check(lib.npr_ctx_set_stats(h, 2))
+    for i in range(3):
+        ws.launch(bufs[i % copies], start=24, endianness=hdr.endianness)
+    ws.check()
+    st = (ctypes.c_uint32 * 8)()
+    ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
+    ntl = ctypes.c_uint64(0)
+    ws.ctx.check(lib.npr_ctx_read_stamps(h, None, 0, ctypes.byref(ntl)))
+    nt = ntl.value
+    stamps = np.zeros(nt * 16, dtype=np.uint64)
+    ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 16))
+    print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} tiles={nt}", file=sys.stderr, flush=True)
+    ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
+
+
+def base_line(args, world, wall, n_per_gpu, bytes_per_gpu):
+    ms_per_step = wall * 1e3 / args.steps
+    total = n_per_gpu * world * args.steps
+    workload = {
+        "c2": "C2: 1M x 64-B Ethernet/IPv4/TCP records per GPU, device-resident",
+        "c3": "C3: 8M records, frames U[64,1500] B, IPv4 TCP|UDP per GPU, device-resident",
+        "c4": "C4: 64M x 64-B records sharded by record range, 8M per GPU (N=8 = configs[3]), device-resident",
+    }[args.config]
+    return {
+        "metric": METRIC,
+        "value": round(total / wall / 1e6, 3),
+        "unit": "Mpackets/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (numpy PCG64 seed 0x4E50; layouts of SURVEY.md 8d)",
+        "config": {"workload": workload,
+                   "outputs": "convert_records flow table (32 B/flow incl. record offset)"},
+        "stream_GBps": round(bytes_per_gpu * world * args.steps / wall / 1e9, 2),
+    }
+
+
+def run_sharded(args, dev, local, rank, world):
+    """c4 over N ranks: rank g holds records [g*R, (g+1)*R) of one capture (only those bytes)."""
+    R = args.records or C4_PER_GPU
+    n_total = R * world
+    layout = parallel.record_range_shards(n_total, world)
+    base, start, stop, spec = layout[rank]
+    a = synth.fixed64_range(R * rank, R * (rank + 1))
+    file_len = 24 + 80 * n_total
+    buf = torch.from_numpy(a).to(dev)
+    del a
+    bounds = [(24 if g == 0 else layout[g][1], layout[g][2]) for g in range(world)]
+    ws = device.Workspace(record_cap=1, flow_cap=R, device=local, records=False, offsets=False, status=False,
+                          flows=True, flows_v6=False)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    # C4 frames are IPv4 by construction: no IPv6 side table to move (pass ws.flows_v6 rows otherwise)
+    step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000)
+    metas, live, rounds = step.step()
+    _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
+    assert rounds == 1 and r_tot == n_total and f_tot == n_total, (rounds, r_tot, f_tot)
+    for _ in range(args.warmup):
+        step.step()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step.step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    # the device time of this rank's launches alone (one event pair per launch series)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    kms = []
+    for _ in range(3):
+        ev0.record(stream)
+        step._launch(step.start if rank == 0 else bounds[rank][0], rank > 0)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        kms.append(ev0.elapsed_time(ev1))
+    kern_ms = float(np.median(kms))
+    step.step()
+    # the flow-table gather to rank 0 (RCCL point-to-point into the merged table), timed apart
+    gms = []
+    for _ in range(max(1, min(3, args.steps))):
+        dist.barrier()
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        fl, _ = step.rows()
+        merged, _ = parallel.gather_flow_tables(fl, None, metas, live)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gms.append((time.perf_counter() - g0) * 1e3)
     if rank == 0:
-        ms_per_step = wall * 1e3 / args.steps
-        total_records = n * world * args.steps
-        value = total_records / wall / 1e6
-        stream_bytes = len(blob) - 24                       # sum(16 + incl_len) per capture
-        read_b = len(blob)                                  # every byte of the capture is read (C2:
-        # = SURVEY 8d's 16 + min(incl, 64) per record; C3: the tiles stream whole payloads too)
-        write_b = 32 * n_flows                              # one 32-B npr_flow per Ok record
-        alg = read_b + write_b
-        achieved = alg / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(n) if not c3 else (None, None)
-        out = {
-            "metric": METRIC,
-            "value": round(value, 3),
-            "unit": "Mpackets/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8",
-            "data": "synthetic (numpy PCG64 seed 0x4E50; C2 layout of SURVEY.md 8d)",
-            "config": {"workload": ("C3: 8M records, frames U[64,1500] B, IPv4 TCP|UDP per GPU, device-resident"
-                                    if c3 else "C2: 1M x 64-B Ethernet/IPv4/TCP records per GPU, device-resident"),
-                       "records_per_gpu": n, "capture_bytes": len(blob), "parallelism": f"record-range x{world}",
-                       "outputs": "convert_records flow table (32 B/flow incl. record offset)"},
-            "stream_GBps": round(stream_bytes * world * args.steps / wall / 1e9, 2),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
-                         "read_only_frac": round(read_b / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                         "bytes_per_launch": alg, "kernel_ms": round(kern_ms, 5)},
-        }
-        if not args.no_cpu and not c3:
-            out["cpu_baseline"] = cpu_baseline(blob, n, args.cpu_budget)
+        assert merged.numel() == 32 * n_total
+        # rows of the merged table run from the last record to the first: check both ends
+        first = merged[:32].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
+        last = merged[-32:].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
+        off = lambda r: int.from_bytes(bytes(r["record_offset"]), "little")
+        assert off(first) == file_len - 80 and off(last) == 24
+    t = torch.tensor([wall, kern_ms, float(np.median(gms))], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_ms, gather_ms = float(t[0]), float(t[1]), float(t[2])
+    out = base_line(args, world, wall, R, len(buf))
+    out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
+    out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
+    step_ms = wall * 1e3 / args.steps
+    out["exchange"] = {"collective": "RCCL all_gather of device summaries (one per step)", "rounds": rounds}
+    out["gather_ms"] = round(gather_ms, 3)
+    out["gather"] = ("RCCL point-to-point of every rank's flow rows straight into rank 0's merged "
+                     f"convert_records table ({32 * n_total / 1e9:.2f} GB)")
+    out["end_to_end_Mpps"] = round(n_total / ((step_ms + gather_ms) * 1e-3) / 1e6, 3)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", choices=["c2", "c3", "c4"], default=None,
+                    help="c2 (N=1 default: 1M x 64-B records), c3 (8M records U[64,1500] B), "
+                         "c4 (N>1 default: 8M x 64-B records per GPU, one capture sharded by record range)")
+    ap.add_argument("--records", type=int, default=None)
+    ap.add_argument("--copies", type=int, default=None)
+    ap.add_argument("--cpu-budget", type=float, default=8.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config is None:
+        args.config = "c2" if world == 1 else "c4"
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        if args.config != "c4":
+            raise SystemExit("N > 1 runs the sharded C4 workload (--config c4)")
+        out = run_sharded(args, dev, local, rank, world)
+    else:
+        out = run_single(args, dev, local)
+    if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

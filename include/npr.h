@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NPR_ABI_VERSION 2
+#define NPR_ABI_VERSION 3
 
 /* ---- status of an API call ------------------------------------------------------------ */
 typedef enum npr_status {
@@ -291,6 +291,32 @@ npr_status npr_dev_parse_extract_chain(npr_ctx *ctx, const void *input, uint64_t
 npr_status npr_dev_parse_extract_chunked(npr_ctx *ctx, const void *input, uint64_t len, uint64_t start,
                                          npr_endianness endianness, const npr_dev_outputs *out,
                                          uint64_t chunk_bytes, void *stream);
+/* One shard of a capture held by this device (multi-GPU record-range sharding):
+ * `input` holds FILE bytes [base, base + input_len).  Records that START in [start, stop) are
+ * produced; every offset in the outputs (record offsets, summary->consumed / ->entry) is a file
+ * offset.  The serial chain of PcapRecords::parse (src/record.rs:30-49) crosses shard boundaries:
+ * rank r's exact first record is rank r-1's `consumed`, which the caller learns from one
+ * exchange and checks against summary->entry (speculative_start != 0 lets this shard start
+ * before it is known).  `input` must extend past `stop` to the end of the last record starting
+ * before it (or to the end of the file): a chain that stops before `stop` in a buffer that ends
+ * before the file does means the halo was too short, which the caller checks.
+ * A shard's buffer does not hold the global header, so the speculation context comes from the
+ * caller: usec_magic (the file's magic is 0xA1B2C3D4 in either byte order: ts_usec < 1e6) and
+ * ts_ref (ts_sec of any record of the file, NPR_NO_ENTRY = none).  Flows-only outputs run as
+ * chained resident launches of about chunk_bytes (0 = one launch's register capacity). */
+typedef struct npr_shard {
+  uint64_t base;
+  uint64_t start;
+  uint64_t stop;
+  int32_t speculative_start;
+  int32_t usec_magic;
+  uint64_t ts_ref;
+  uint64_t chunk_bytes;
+} npr_shard;
+
+npr_status npr_dev_parse_extract_shard(npr_ctx *ctx, const void *input, uint64_t input_len,
+                                       npr_endianness endianness, const npr_shard *shard,
+                                       const npr_dev_outputs *out, void *stream);
 /* Synchronise `stream`, copy the summary back and map its flags to a status. */
 npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
                          npr_summary *host_summary);

@@ -140,15 +140,20 @@ static void level_sizes(uint64_t nt, uint64_t n[npr::kLevels + 1]) {
   n[0] = nt;
   for (int l = 1; l <= npr::kLevels; ++l) n[l] = (n[l - 1] + 63) / 64;
 }
-// tile slots, then the level-1..3 group slots: one allocation (granules are epoch-tagged, so the
-// layout may shift between launches)
-static uint64_t slot_bytes(uint64_t nt) {
+// group slots after the tile slots: the two-pass kernels' level-1..3 folds, or the resident pass's
+// one aggregate per workgroup (rgroups = groups[1], up to ceil(min(nt, kResMaxWaves) / kResWgMin)
+// slots, which can exceed the fold levels' ceil(nt/64) + ceil(nt/4096) + ...)
+static uint64_t group_slots(uint64_t nt) {
   uint64_t n[npr::kLevels + 1];
   level_sizes(nt, n);
-  uint64_t b = nt * sizeof(npr::TileSlot);
-  for (int l = 1; l <= npr::kLevels; ++l) b += n[l] * sizeof(npr::GroupSlot);
-  return b;
+  uint64_t folds = 0;
+  for (int l = 1; l <= npr::kLevels; ++l) folds += n[l];
+  const uint64_t res = (std::min<uint64_t>(nt, npr::kResMaxWaves) + npr::kResWgMin - 1) / npr::kResWgMin;
+  return std::max(folds, res);
 }
+// tile slots, then the group slots: one allocation (granules are epoch-tagged, so the layout may
+// shift between launches)
+static uint64_t slot_bytes(uint64_t nt) { return nt * sizeof(npr::TileSlot) + group_slots(nt) * sizeof(npr::GroupSlot); }
 
 uint64_t npr_workspace_bytes(uint64_t len) {
   const uint64_t nt = tiles_for(len, 0, nullptr);
@@ -299,9 +304,22 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
   return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
 }
 
+// A shard's buffer holds file bytes [base, len) only: byte offsets stay file offsets, and the
+// speculation context (the magic's ts_usec bound, a reference ts_sec) comes from the host.
+struct ShardSpec {
+  uint64_t base = 0;
+  uint32_t frac_max = 1000000000u;
+  bool has_ref = false;
+  uint32_t ts_ref = 0;
+};
+
 static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
                                npr_endianness e, int speculative_start, uint64_t ref_record,
-                               const npr_summary *prev, const npr_dev_outputs *o, void *stream);
+                               const npr_summary *prev, const npr_dev_outputs *o, void *stream,
+                               const ShardSpec *sh = nullptr);
+static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                          npr_endianness e, int speculative_start, uint64_t ref_record, const npr_dev_outputs *o,
+                          uint64_t chunk_bytes, void *stream, const ShardSpec *sh);
 
 npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness e, int speculative_start,
@@ -320,29 +338,56 @@ npr_status npr_dev_parse_extract_chunked(npr_ctx *c, const void *input, uint64_t
                                          void *stream) {
   if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
   if (start > len) return fail(c, NPR_ERR_ARG, "need start <= len");
+  return chained(c, input, len, start, len, e, 0, start, o, chunk_bytes, stream, nullptr);
+}
+
+// Records starting in [start, stop) as chained resident launches of about chunk_bytes each (the
+// first one may speculate its start); launches that need a record table / offsets / status run
+// the two-pass kernels in one launch instead.
+static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                          npr_endianness e, int speculative_start, uint64_t ref_record, const npr_dev_outputs *o,
+                          uint64_t chunk_bytes, void *stream, const ShardSpec *sh) {
   const bool flows_only = !o->record_offsets && !o->records && !o->record_status;
-  if (!c->resident || !flows_only)  // the two-pass kernels take any size in one launch
-    return launch_range(c, input, len, start, len, e, 0, start, nullptr, o, stream);
+  if (!c->resident || !flows_only || stop <= start)
+    return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream, sh);
   npr_status st = res_geometry(c);
   if (st) return st;
-  uint64_t chunk = chunk_bytes ? chunk_bytes : (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
+  const uint64_t chunk = chunk_bytes ? chunk_bytes : (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
   if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
   npr_dev_outputs oc = *o;
   const npr_summary *prev = nullptr;
   uint64_t lo = start;
   for (uint64_t k = 0;; ++k) {
-    const uint64_t hi = len - lo <= chunk ? len : lo + chunk;
-    oc.summary = hi == len ? o->summary : (npr_summary *)c->chain.p + (k & 1u);
-    if ((st = launch_range(c, input, len, lo, hi, e, 0, start, prev, &oc, stream))) return st;
-    if (hi == len) return NPR_OK;
+    const uint64_t hi = stop - lo <= chunk ? stop : lo + chunk;
+    oc.summary = hi == stop ? o->summary : (npr_summary *)c->chain.p + (k & 1u);
+    if ((st = launch_range(c, input, len, lo, hi, e, k == 0 ? speculative_start : 0, ref_record, prev, &oc, stream,
+                           sh)))
+      return st;
+    if (hi == stop) return NPR_OK;
     prev = oc.summary;
     lo = hi;
   }
 }
 
+npr_status npr_dev_parse_extract_shard(npr_ctx *c, const void *input, uint64_t input_len, npr_endianness e,
+                                       const npr_shard *shard, const npr_dev_outputs *o, void *stream) {
+  if (!c || !o || !o->summary || !shard || (!input && input_len)) return fail(c, NPR_ERR_ARG, "null argument");
+  const uint64_t len = shard->base + input_len;
+  if (shard->start < shard->base || shard->start > shard->stop || shard->stop > len)
+    return fail(c, NPR_ERR_ARG, "need base <= start <= stop <= base + input_len");
+  ShardSpec sh;
+  sh.base = shard->base;
+  sh.frac_max = shard->usec_magic ? 1000000u : 1000000000u;
+  sh.has_ref = shard->ts_ref != NPR_NO_ENTRY;
+  sh.ts_ref = (uint32_t)shard->ts_ref;
+  return chained(c, input, len, shard->start, shard->stop, e, shard->speculative_start, NPR_NO_ENTRY, o,
+                 shard->chunk_bytes, stream, &sh);
+}
+
 static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
                                npr_endianness e, int speculative_start, uint64_t ref_record,
-                               const npr_summary *prev, const npr_dev_outputs *o, void *stream) {
+                               const npr_summary *prev, const npr_dev_outputs *o, void *stream,
+                               const ShardSpec *sh) {
   if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
   if (stop > len || start > stop) return fail(c, NPR_ERR_ARG, "need start <= stop <= len");
   if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
@@ -350,8 +395,11 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     return fail(c, NPR_ERR_ARG, "flow arrays must be 16-byte aligned");
   if (len >= (1ull << 40)) return fail(c, NPR_ERR_ARG, "input larger than 1 TiB (40-bit record offsets)");
   HIP_CHECK(c, hipSetDevice(c->device));
+  const uint64_t base = sh ? sh->base : 0;
+  if (start < base) return fail(c, NPR_ERR_ARG, "need start >= base");
   uint64_t org = 0;
-  const uint64_t nt = tiles_for(stop, start, &org);  // tiles cover [org, stop)
+  const uint64_t nt = tiles_for(stop - base, start - base, &org);  // tiles cover [org, stop)
+  org += base;
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
   npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
   if (st) return st;
@@ -363,7 +411,8 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, kCtlBytes, s));
   }
   npr::ParseParams p{};
-  p.buf = (const uint8_t *)input;
+  p.buf = (const uint8_t *)input - base;  // buf + o = file byte o (only o >= base is ever read)
+  p.base = base;
   p.len = len;
   p.start = start;
   p.org = org;
@@ -376,6 +425,12 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
   // a capture file: bytes 0..3 hold the pcap magic (the kernel checks its value)
   p.flags = (start >= 24 || (ref_record != NPR_NO_ENTRY && ref_record >= 24)) ? npr::kFlagMagicAtZero : 0u;
   if (speculative_start) p.flags |= npr::kFlagSpecStart;
+  if (sh) {  // a shard: bytes 0..3 (the magic) and the first record are not in its buffer
+    p.flags = (p.flags & ~npr::kFlagMagicAtZero) | npr::kFlagHostSpec | (sh->has_ref ? npr::kFlagHostRef : 0u);
+    p.frac_max = sh->frac_max;
+    p.ts_ref = sh->ts_ref;
+    p.ref = ~0ull;
+  }
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
   uint64_t nl[npr::kLevels + 1];
@@ -423,6 +478,11 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.nwaves = (uint32_t)wv;
     p.rslots = (npr::RangeSlot *)c->slots.p;
     p.rgroups = p.groups[1];
+    // every workgroup aggregate the launch writes must lie inside the slot allocation
+    const uint64_t nb = (wv + npr::kResWgMin - 1) / npr::kResWgMin;
+    if ((const char *)(p.rgroups + nb) > (const char *)c->slots.p + c->slots.cap)
+      return fail(c, NPR_ERR_ARG, "internal: resident workgroup slots exceed the workspace (%llu groups)",
+                  (unsigned long long)nb);
     const uint64_t bank = c->res_launches++ & 1u;  // this launch counts in a bank the previous one zeroed
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters + bank * kCtlBank);
     p.rcnt_next = (uint32_t *)((char *)c->abort_word + kCtlCounters + (bank ^ 1u) * kCtlBank);

@@ -67,6 +67,8 @@ constexpr int kLevels = 3;  // group levels above the tiles
 enum : uint32_t {
   kFlagMagicAtZero = 2u,  // buf[0..4) is the pcap magic (start >= 24): tighten ts_usec bound
   kFlagSpecStart = 8u,    // `start` is not a known record boundary: speculate tile 0's entry too
+  kFlagHostSpec = 16u,    // a shard (buf does not hold bytes 0..3): frac_max / ts_ref come from the host
+  kFlagHostRef = 32u,     //   ... and ts_ref is valid
 };
 
 // optional diagnostic counters (ParseParams::stats, NULL in production launches)
@@ -80,7 +82,9 @@ enum : uint32_t {
 constexpr int kStampWords = 16;  // diagnostic stamps per tile (npr_ctx_read_stamps)
 
 struct ParseParams {
-  const uint8_t *buf;  // 16-B aligned device pointer
+  // Every offset below is a FILE offset.  buf + o addresses file byte o; the caller's buffer holds
+  // file bytes [base, len) (base = 0 except for a shard), so buf itself may point before it.
+  const uint8_t *buf;  // caller pointer - base (caller pointer 16-B aligned)
   uint64_t len;
   uint64_t start;      // offset of the first record (or where to speculate it, kFlagSpecStart)
   uint64_t stop;       // only records starting before `stop` belong to this launch (<= len)
@@ -92,6 +96,8 @@ struct ParseParams {
   uint32_t frac_max;   // speculation bound on ts_usec (1e9 accepts ns captures)
   uint32_t flags;
   uint32_t timeout_ticks;  // s_memrealtime (100 MHz) ticks before a stalled hand-off aborts
+  uint32_t ts_ref;         // kFlagHostRef: ts_sec of a known record of the capture (speculation anchor)
+  uint64_t base;           // file offset of the caller's first byte (tiles start at org >= base)
   TileSlot *slots;
   GroupSlot *groups[kLevels + 1];  // [1..3]; [0] unused
   uint32_t ngroups[kLevels + 1];   // [0] = ntiles, [l] = ceil(ngroups[l-1] / 64)

@@ -896,6 +896,7 @@ typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
 // reference record's ts_sec (range-checked: a byte outside the input reads 0).  spec_ctx()
 // finishes it once the loads landed.
 __device__ __forceinline__ uint32_t spec_ctx_load(const ParseParams &kp) {
+  if (kp.flags & kFlagHostSpec) return 0u;  // a shard: bytes 0..3 are not in its buffer
   const uint32_t lane = threadIdx.x & 63u;
   const bool has_ref = kp.ref != kNone && kp.len >= kp.ref + 16;
   const uint64_t lim = kp.len < 0x7fffffffull ? kp.len : 0x7fffffffull;
@@ -909,6 +910,14 @@ __device__ __forceinline__ uint32_t spec_ctx_load(const ParseParams &kp) {
 __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp, uint32_t b) {
   SpecCtx sc;
   sc.big = kp.big;
+  sc.avail = 0;
+  sc.exact_end = true;
+  if (kp.flags & kFlagHostSpec) {  // a shard: the host supplies the magic's bound and the reference ts_sec
+    sc.frac_max = kp.frac_max;
+    sc.has_ref = (kp.flags & kFlagHostRef) != 0;
+    sc.ts_ref = kp.ts_ref;
+    return sc;
+  }
   uint32_t v = b << (8 * (threadIdx.x & 3u));
   v |= __shfl_xor((int)v, 1, 64);
   v |= __shfl_xor((int)v, 2, 64);
@@ -918,8 +927,6 @@ __device__ __forceinline__ SpecCtx spec_ctx(const ParseParams &kp, uint32_t b) {
   sc.frac_max = ((kp.flags & kFlagMagicAtZero) && (m == 0xA1B2C3D4u || m == 0xD4C3B2A1u)) ? 1000000u : kp.frac_max;
   sc.has_ref = kp.ref != kNone && kp.len >= kp.ref + 16;
   sc.ts_ref = kp.big ? __builtin_bswap32(r) : r;
-  sc.avail = 0;
-  sc.exact_end = true;
   return sc;
 }
 

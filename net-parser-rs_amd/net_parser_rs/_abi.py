@@ -74,13 +74,19 @@ class DevOutputsC(ctypes.Structure):
                 ("summary", ctypes.c_void_p)]
 
 
+class ShardC(ctypes.Structure):
+    _fields_ = [("base", ctypes.c_uint64), ("start", ctypes.c_uint64), ("stop", ctypes.c_uint64),
+                ("speculative_start", ctypes.c_int32), ("usec_magic", ctypes.c_int32),
+                ("ts_ref", ctypes.c_uint64), ("chunk_bytes", ctypes.c_uint64)]
+
+
 class SummaryC(ctypes.Structure):
     _fields_ = [("n_records", ctypes.c_uint64), ("n_flows", ctypes.c_uint64),
                 ("consumed", ctypes.c_uint64), ("flags", ctypes.c_uint32),
                 ("epoch", ctypes.c_uint32), ("entry", ctypes.c_uint64)]
 
 
-assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24
+assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24 and ctypes.sizeof(ShardC) == 48
 
 # Every symbol include/npr.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -89,7 +95,7 @@ EXPORTED = [
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
-    "npr_dev_parse_extract_chunked", "npr_dev_check", "npr_dev_extract_flows",
+    "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -129,6 +135,8 @@ _SIGNATURES = {
                                                    ctypes.POINTER(DevOutputsC), _vp]),
     "npr_dev_parse_extract_chunked": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                                      ctypes.POINTER(DevOutputsC), ctypes.c_uint64, _vp]),
+    "npr_dev_parse_extract_shard": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ShardC),
+                                                   ctypes.POINTER(DevOutputsC), _vp]),
     "npr_dev_check": (ctypes.c_int, [_vp, ctypes.POINTER(DevOutputsC), _vp, ctypes.POINTER(SummaryC)]),
     "npr_dev_extract_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                              _vp, _vp, _vp, _vp]),

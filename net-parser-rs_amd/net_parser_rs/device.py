@@ -18,9 +18,9 @@ from . import _abi, context
 
 class Workspace:
     def __init__(self, record_cap, flow_cap, device=0, records=True, offsets=False, status=False,
-                 flows=True, flows_v6=True):
+                 flows=True, flows_v6=True, ctx=None):
         self.device = torch.device("cuda", device)
-        self.ctx = context(device)
+        self.ctx = ctx if ctx is not None else context(device)  # a Context is per thread (npr_ctx)
         self.record_cap, self.flow_cap = int(record_cap), int(flow_cap)
         mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=self.device)
         self.records = mk(self.record_cap * 24) if records else None
@@ -69,6 +69,28 @@ class Workspace:
                                                         ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
+
+    def launch_shard(self, buf, base, start, stop, endianness=_abi.LITTLE, speculative=False, usec_magic=True,
+                     ts_ref=None, chunk_bytes=0, nbytes=None, stream=None):
+        """One shard held by this device (npr_dev_parse_extract_shard): `buf` holds FILE bytes
+        [base, base + nbytes); records that START in [start, stop) are produced, with file offsets.
+        usec_magic / ts_ref: the capture's speculation context (its buffer lacks the header)."""
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        n = buf.numel() if nbytes is None else int(nbytes)
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        sh = _abi.ShardC(int(base), int(start), int(stop), 1 if speculative else 0, 1 if usec_magic else 0,
+                         _abi.NO_ENTRY if ts_ref is None else int(ts_ref), int(chunk_bytes))
+        st = self.ctx.lib.npr_dev_parse_extract_shard(self.ctx.handle, buf.data_ptr(), n, endianness, ctypes.byref(sh),
+                                                      ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        self.ctx.check(st)
+        self._stream = s
+
+    def flow_rows(self, n_flows=None):
+        """The right-aligned flow rows as device tensors (views, no copy): (flows, flows_v6)."""
+        k = min(self.last.n_flows if n_flows is None else int(n_flows), self.flow_cap)
+        lo, hi = (self.flow_cap - k) * 32, self.flow_cap * 32
+        return (self.flows[lo:hi] if self.flows is not None else None,
+                self.flows_v6[lo:hi] if self.flows_v6 is not None else None)
 
     def check(self):
         sm = _abi.SummaryC()

@@ -13,10 +13,13 @@ starts where record k ends, and the list stops at the first Incomplete record (Q
 4. a chain END (an Incomplete record) inside rank r's range ends the whole capture there:
    later ranks contribute nothing, exactly as the serial reference stops;
 5. flows are gathered to the root in REVERSE rank order, which is convert_records' order
-   (src/flow/mod.rs:101-123: reverse file order).
+   (src/flow/mod.rs:101-123: reverse file order): point-to-point transfers of each rank's rows
+   (and IPv6 side rows) straight into their place in the root's table — RCCL over xGMI for device
+   tensors, gloo for host tensors.
 
-The local parse is a callback (`LocalParse`), so the same reconcile logic drives the device path
-(`device_local`) and the CPU tests (tests/test_parallel.py, gloo, the oracle as the local parser).
+The local parse is a callback (`LocalParse`), so the same reconcile logic drives the device paths
+(`shard_local`: a rank holds only its shard, npr_dev_parse_extract_shard; `device_local`: the whole
+capture in one HBM) and the CPU tests (tests/test_parallel.py, gloo, the oracle as the local parser).
 """
 from dataclasses import dataclass
 from typing import Callable, List, Optional
@@ -40,8 +43,8 @@ class ShardResult:
     consumed: int     # where the chain leaves the range (>= hi), or the END position (< hi)
     n_records: int
     n_flows: int
-    flows: Optional[np.ndarray] = None      # FLOW_DTYPE rows, convert_records order (reverse)
-    flows_v6: Optional[np.ndarray] = None
+    flows: Optional[object] = None      # FLOW_DTYPE rows (numpy), or their bytes as a device tensor
+    flows_v6: Optional[object] = None   # the IPv6 side rows, same form
 
 
 # local(lo, hi, start, speculative) -> ShardResult for the records starting in [start, hi)
@@ -77,18 +80,20 @@ def exact_result(local: LocalParse, lo: int, hi: int, e: int) -> ShardResult:
     return local(lo, hi, e, False)
 
 
-def parse_sharded_inprocess(local: LocalParse, start: int, length: int, world: int):
+def parse_sharded_inprocess(local, start: int, length: int, world: int, bounds=None):
     """Every shard in this process (one GPU, or the CPU tests): same reconcile as the
-    distributed form.  Returns (results, live, rounds)."""
-    bounds = shard_bounds(start, length, world)
-    results = [local(lo, hi, lo, r > 0) if r > 0 else local(lo, hi, start, False)
+    distributed form.  `local` is one LocalParse for all ranks, or a list of one per rank (each
+    rank's shard in its own buffer).  Returns (results, live, rounds)."""
+    bounds = bounds or shard_bounds(start, length, world)
+    locals_ = local if isinstance(local, (list, tuple)) else [local] * world
+    results = [locals_[r](lo, hi, lo, True) if r > 0 else locals_[r](lo, hi, start, False)
                for r, (lo, hi) in enumerate(bounds)]
     rounds = 1
     while True:
         bad, e, live = replay(start, bounds, results)
         if bad is None:
             return results, live, rounds
-        results[bad] = exact_result(local, *bounds[bad], e)
+        results[bad] = exact_result(locals_[bad], *bounds[bad], e)
         rounds += 1
 
 
@@ -104,12 +109,12 @@ def _gather_meta(res: ShardResult, group, device):
                         n_records=int(t[2]), n_flows=int(t[3])) for t in (x.cpu() for x in out)]
 
 
-def parse_sharded(local: LocalParse, start: int, length: int, group=None, device="cpu"):
+def parse_sharded(local: LocalParse, start: int, length: int, group=None, device="cpu", bounds=None):
     """Distributed form: this rank parses its range; one all-gather per round reconciles.
     Returns (my_result, metas, live, rounds); `metas` are every rank's final counts."""
     import torch.distributed as dist
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    bounds = shard_bounds(start, length, world)
+    bounds = bounds or shard_bounds(start, length, world)
     lo, hi = bounds[rank]
     mine = local(lo, hi, lo, True) if rank > 0 else local(lo, hi, start, False)
     rounds = 1
@@ -135,33 +140,102 @@ def prefix_offsets(metas: List[ShardResult], live):
     return rec_off, flow_off, r_tot, f_tot
 
 
+def merged_positions(metas: List[ShardResult], live):
+    """Row of each live rank's first flow in the merged convert_records table (reverse file order:
+    the LAST rank's flows come first, src/flow/mod.rs:101-123), and the total."""
+    pos, p = {}, 0
+    for r in reversed(range(len(metas))):
+        if live[r] and metas[r].n_flows:
+            pos[r] = p
+            p += metas[r].n_flows
+    return pos, p
+
+
 def merge_flows(results: List[ShardResult], live):
-    """convert_records order over the whole capture: the ranks' tables in reverse rank order."""
-    parts = [res.flows for res, ok in zip(results[::-1], live[::-1]) if ok and res.n_flows]
-    return np.concatenate(parts) if parts else np.zeros(0, _abi.FLOW_DTYPE)
+    """convert_records order over the whole capture: the ranks' tables in reverse rank order.
+    Returns (flows, flows_v6); flows_v6 is None unless every contributing rank has one."""
+    parts = [res for res, ok in zip(results[::-1], live[::-1]) if ok and res.n_flows]
+    flows = np.concatenate([r.flows for r in parts]) if parts else np.zeros(0, _abi.FLOW_DTYPE)
+    if parts and all(r.flows_v6 is not None for r in parts):
+        v6 = np.concatenate([r.flows_v6 for r in parts])
+    else:
+        v6 = None if parts else np.zeros(0, _abi.FLOW_V6_DTYPE)
+    return flows, v6
+
+
+def _as_bytes_tensor(x):
+    import torch
+    if x is None:
+        return None
+    if isinstance(x, np.ndarray):
+        return torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1).copy())
+    return x.contiguous().view(-1)
+
+
+def gather_flow_tables(flows, flows_v6, metas: List[ShardResult], live, group=None, dst=0):
+    """Gather every rank's flow rows to `dst` by point-to-point transfers straight into their
+    place in the merged table (no padding, no concatenation pass): rank r's rows land at
+    merged_positions()[r].  `flows` / `flows_v6` are this rank's n_flows rows as uint8 tensors
+    (n_flows * 32 bytes) on the backend's device: CUDA tensors over RCCL (xGMI), CPU tensors over
+    gloo; flows_v6 may be None (then no side table is gathered).  Returns (merged, merged_v6)
+    uint8 tensors on dst, (None, None) elsewhere."""
+    import torch
+    import torch.distributed as dist
+    rank = dist.get_rank(group)
+    pos, total = merged_positions(metas, live)
+    with_v6 = flows_v6 is not None
+    gr = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    reqs = []
+    if rank != dst:
+        if rank in pos:
+            n = metas[rank].n_flows
+            reqs.append(dist.isend(flows[: n * 32].contiguous(), gr(dst), group=group))
+            if with_v6:
+                reqs.append(dist.isend(flows_v6[: n * 32].contiguous(), gr(dst), group=group))
+        for q in reqs:
+            q.wait()
+        return None, None
+    dev = flows.device if flows is not None else "cpu"
+    out = torch.empty(max(total, 1) * 32, dtype=torch.uint8, device=dev)[: total * 32]
+    out6 = torch.empty(max(total, 1) * 32, dtype=torch.uint8, device=dev)[: total * 32] if with_v6 else None
+    for r, p in sorted(pos.items()):
+        n = metas[r].n_flows
+        sl = slice(p * 32, (p + n) * 32)
+        if r == rank:
+            out[sl].copy_(flows[: n * 32])
+            if with_v6:
+                out6[sl].copy_(flows_v6[: n * 32])
+        else:
+            reqs.append(dist.irecv(out[sl], gr(r), group=group))
+            if with_v6:
+                reqs.append(dist.irecv(out6[sl], gr(r), group=group))
+    for q in reqs:
+        q.wait()
+    return out, out6
 
 
 def gather_flows(mine: ShardResult, metas: List[ShardResult], live, group=None, dst=0):
-    """Gather every rank's flow rows to `dst` (padded to the largest count) and merge there."""
-    import torch
+    """gather_flow_tables over this rank's rows (numpy or tensors); on dst returns the merged
+    (flows, flows_v6) as numpy record arrays (flows_v6 None when the ranks hold none)."""
     import torch.distributed as dist
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
-    width = max([m.n_flows for m in metas] + [1])
-    buf = torch.zeros(width * 32, dtype=torch.uint8)
-    if live[rank] and mine.n_flows:
-        buf[: mine.n_flows * 32] = torch.from_numpy(mine.flows.view(np.uint8).copy())
-    bufs = [torch.zeros_like(buf) for _ in range(world)] if rank == dst else None
-    dist.gather(buf, bufs, dst=dst, group=group)
-    if rank != dst:
+    rank = dist.get_rank(group)
+    ok = live[rank] and mine.n_flows
+    fl = _as_bytes_tensor(mine.flows) if ok else None
+    v6 = _as_bytes_tensor(mine.flows_v6) if ok else None
+    if fl is None:
+        import torch
+        fl = torch.zeros(0, dtype=torch.uint8)
+    # every rank must agree on whether a side table moves: gather it when this rank has one
+    out, out6 = gather_flow_tables(fl, v6 if mine.flows_v6 is not None else None, metas, live, group=group, dst=dst)
+    if out is None:
         return None
-    rows = [ShardResult(m.entry, m.consumed, m.n_records, m.n_flows,
-                        flows=b[: m.n_flows * 32].numpy().view(_abi.FLOW_DTYPE)) for m, b in zip(metas, bufs)]
-    return merge_flows(rows, live)
+    f = out.cpu().numpy().view(_abi.FLOW_DTYPE)
+    return f, (out6.cpu().numpy().view(_abi.FLOW_V6_DTYPE) if out6 is not None else None)
 
 
 def device_local(ws, buf, length, endianness=_abi.LITTLE, ref_record=24) -> LocalParse:
     """The product's local parser: npr_dev_parse_extract_range on this rank's GPU (`ws` a
-    device.Workspace, `buf` the capture — or this rank's range plus a halo — in HBM)."""
+    device.Workspace, `buf` the whole capture in HBM).  Results are copied to the host."""
     def local(lo, hi, start, speculative):
         ws.launch_range(buf, start, hi, endianness=endianness, speculative=speculative,
                         ref_record=ref_record, nbytes=length)
@@ -171,3 +245,113 @@ def device_local(ws, buf, length, endianness=_abi.LITTLE, ref_record=24) -> Loca
         return ShardResult(entry=int(sm.entry), consumed=int(sm.consumed), n_records=int(sm.n_records),
                            n_flows=int(sm.n_flows), flows=flows, flows_v6=v6)
     return local
+
+
+class HaloError(RuntimeError):
+    """A shard's chain stopped at a record whose bytes run past the shard's buffer (not the end of
+    the file): the buffer needs a longer halo."""
+
+
+def shard_local(ws, buf, base, file_len, endianness=_abi.LITTLE, usec_magic=True, ts_ref=None,
+                nbytes=None, chunk_bytes=0, to_host=False) -> LocalParse:
+    """The product's local parser over a SHARD held by this device (npr_dev_parse_extract_shard):
+    `buf` holds file bytes [base, base + nbytes).  Flow rows stay in HBM (device tensor views of
+    the workspace, or host copies with to_host=True)."""
+    n = buf.numel() if nbytes is None else int(nbytes)
+
+    def local(lo, hi, start, speculative):
+        ws.launch_shard(buf, base, start, hi, endianness=endianness, speculative=speculative,
+                        usec_magic=usec_magic, ts_ref=ts_ref, chunk_bytes=chunk_bytes, nbytes=n)
+        sm = ws.check()
+        if sm.consumed < hi and base + n < file_len and sm.entry != NO_ENTRY:
+            incl_end = sm.consumed  # the chain stopped inside the shard: is it the file's end?
+            raise HaloError(f"shard [{base}, {base + n}) of a {file_len}-byte capture ends a chain at "
+                            f"{incl_end} < stop {hi}: extend its buffer past the last record")
+        if to_host:
+            fl, v6 = ws.flows_np().copy(), (ws.flows_v6_np().copy() if ws.flows_v6 is not None else None)
+        else:
+            fl, v6 = ws.flow_rows(sm.n_flows)
+        return ShardResult(entry=int(sm.entry), consumed=int(sm.consumed), n_records=int(sm.n_records),
+                           n_flows=int(sm.n_flows), flows=fl, flows_v6=v6)
+    return local
+
+
+def record_range_shards(n_records, world, record_bytes=80, header=24):
+    """C4 layout: a fixed-stride capture of n_records split by record range, rank g
+    holding records [g*R, (g+1)*R): returns per rank (base, start, stop, speculative) in file
+    offsets, rank 0's buffer starting at byte 0 (the global header)."""
+    out = []
+    for g in range(world):
+        r0, r1 = n_records * g // world, n_records * (g + 1) // world
+        lo, hi = header + record_bytes * r0, header + record_bytes * r1
+        out.append((0 if g == 0 else lo, header if g == 0 else lo, hi, g > 0))
+    return out
+
+
+class DeviceShardedParse:
+    """The device-resident multi-GPU step (C4 / C5, SURVEY.md 8 row e), one rank per GPU:
+
+      launch this rank's shard (npr_dev_parse_extract_shard, chained resident launches) ->
+      ONE RCCL all-gather of every rank's device summary {n_records, n_flows, consumed, entry}
+      straight from HBM (stream-ordered behind the parse, no host round trip in between) ->
+      replay the serial chain on the host; a rank whose speculated entry is contradicted re-parses
+      from the exact one and the exchange repeats (never with a plausible speculation).
+
+    The flow rows stay in this rank's HBM (`rows()`) until gather_flow_tables() moves them.
+    `bounds` are every rank's (lo, hi) record-start ranges; this rank's buffer holds file bytes
+    [base, base + nbytes)."""
+
+    def __init__(self, ws, buf, base, bounds, file_len, endianness=_abi.LITTLE, usec_magic=True, ts_ref=None,
+                 start=24, group=None, nbytes=None, chunk_bytes=0):
+        import torch
+        import torch.distributed as dist
+        self.ws, self.buf, self.base, self.bounds = ws, buf, int(base), bounds
+        self.file_len, self.e, self.usec, self.ts_ref = int(file_len), endianness, usec_magic, ts_ref
+        self.start, self.group = int(start), group
+        self.nbytes = buf.numel() if nbytes is None else int(nbytes)
+        self.chunk = int(chunk_bytes)
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.gathered = torch.zeros(self.world * ws.summary.numel(), dtype=torch.uint8, device=ws.summary.device)
+
+    def _launch(self, start, speculative):
+        lo, hi = self.bounds[self.rank]
+        self.ws.summary.zero_()  # an unwritten summary (a launch that did not complete) reads epoch 0
+        self.ws.launch_shard(self.buf, self.base, start, hi, endianness=self.e, speculative=speculative,
+                             usec_magic=self.usec, ts_ref=self.ts_ref, chunk_bytes=self.chunk, nbytes=self.nbytes)
+
+    def _exchange(self):
+        import torch.distributed as dist
+        dist.all_gather_into_tensor(self.gathered, self.ws.summary, group=self.group)
+        g = self.gathered.cpu().numpy().reshape(self.world, -1)[:, :40].copy().view(_abi.SUMMARY_DTYPE).reshape(-1)
+        if (g["epoch"] == 0).any() or (g["flags"] != 0).any():
+            bad = [int(r) for r in range(self.world) if g["epoch"][r] == 0 or g["flags"][r] != 0]
+            raise RuntimeError(f"shard parse did not complete or overflowed on ranks {bad}")
+        return [ShardResult(entry=int(x["entry"]), consumed=int(x["consumed"]), n_records=int(x["n_records"]),
+                            n_flows=int(x["n_flows"])) for x in g]
+
+    def step(self):
+        """-> (metas, live, rounds).  Raises HaloError when a chain stops short of a buffer end."""
+        lo, hi = self.bounds[self.rank]
+        self._launch(self.start if self.rank == 0 else lo, self.rank > 0)
+        rounds = 1
+        while True:
+            metas = self._exchange()
+            bad, e, live = replay(self.start, self.bounds, metas)
+            if bad is None:
+                break
+            if bad == self.rank:
+                if e >= hi:
+                    raise HaloError(f"rank {self.rank}: a record spans the whole shard; not supported by the device step")
+                self._launch(e, False)
+            else:  # keep the stream order: an empty launch is not needed, the others just re-gather
+                pass
+            rounds += 1
+        m = metas[self.rank]
+        if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
+            raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
+        self.metas, self.live = metas, live
+        return metas, live, rounds
+
+    def rows(self):
+        m = self.metas[self.rank]
+        return self.ws.flow_rows(m.n_flows if self.live[self.rank] else 0)

@@ -55,6 +55,50 @@ def fixed64(n, seed=SEED, with_header=True):
     return (global_header() + body.tobytes()) if with_header else body.tobytes()
 
 
+BLOCK = 1 << 20  # records per independently seeded block (fixed64_range)
+
+
+def _fixed64_block(k, seed):
+    """Block k of the shard-independent C2-shape stream: records [k*BLOCK, (k+1)*BLOCK)."""
+    rng = np.random.default_rng([seed, 4, k])
+    n = BLOCK
+    rec = rng.integers(0, 256, size=(n, 80), dtype=np.uint8)
+    i = np.arange(k * BLOCK, (k + 1) * BLOCK, dtype=np.int64)
+    hdr = np.empty((n, 4), dtype="<u4")
+    hdr[:, 0] = (1_600_000_000 + i // 1_000_000).astype(np.uint32)
+    hdr[:, 1] = (i % 1_000_000).astype(np.uint32)
+    hdr[:, 2] = 64
+    hdr[:, 3] = 64
+    rec[:, 0:16] = hdr.view(np.uint8).reshape(n, 16)
+    f = rec[:, 16:]
+    f[:, 12] = 0x08; f[:, 13] = 0x00
+    f[:, 14] = 0x45; f[:, 15] = 0x00
+    f[:, 16] = 0x00; f[:, 17] = 50
+    f[:, 20] = 0x00; f[:, 21] = 0x00
+    f[:, 22] = 64; f[:, 23] = 6
+    flags = rng.integers(0, 512, size=n, dtype=np.uint16)
+    hv = (5 << 12) | flags
+    f[:, 46] = (hv >> 8).astype(np.uint8); f[:, 47] = (hv & 0xff).astype(np.uint8)
+    return rec
+
+
+def fixed64_range(lo, hi, seed=SEED):
+    """Records [lo, hi) of the C4 capture (64M x C2-shape records; shard-independent:
+    record i's bytes depend only on i, through per-block seeding, so a rank generates exactly its
+    own range).  Returns the bytes of file range [24 + 80*lo, 24 + 80*hi), preceded by the global
+    header when lo == 0 (then the buffer starts at file byte 0), as a numpy uint8 array."""
+    h = 24 if lo == 0 else 0
+    out = np.empty(h + 80 * (hi - lo), dtype=np.uint8)
+    if h:
+        out[:24] = np.frombuffer(global_header(), dtype=np.uint8)
+    for k in range(lo // BLOCK, (hi + BLOCK - 1) // BLOCK):
+        b = _fixed64_block(k, seed)
+        a, z = max(lo, k * BLOCK) - k * BLOCK, min(hi, (k + 1) * BLOCK) - k * BLOCK
+        o = h + 80 * (k * BLOCK + a - lo)
+        out[o: o + 80 * (z - a)] = b[a:z].reshape(-1)
+    return out
+
+
 def variable_mix(n, seed=SEED + 3, with_header=True):
     """C3: n records, frame length U[64, 1500], IPv4 + (TCP | UDP)."""
     rng = np.random.default_rng(seed)

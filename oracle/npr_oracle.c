@@ -391,3 +391,83 @@ size_t or_bench_extract(const uint8_t *in, size_t len, npr_record *rec_scratch, 
   if (n > rec_cap) n = rec_cap;
   return or_convert_records(in, len, rec_scratch, n, flow_scratch, v6_scratch, flow_cap);
 }
+
+/* ---- bench leg on T host threads: the same CaptureFile::parse + convert_records result ------
+ * The record chain is walked serially (it IS serial: src/record.rs:30-49, and cheap); the
+ * extract_flow tree, which is ~85 % of the reference's `extract` time (benches/benches.rs:80-81),
+ * runs on T threads over contiguous record ranges; every thread then writes its Ok flows to
+ * their reverse-order rows from a prefix of the per-thread counts (src/flow/mod.rs:101-123). */
+#include <pthread.h>
+
+typedef struct {
+  const uint8_t *in;
+  size_t len;
+  const npr_record *recs;
+  size_t lo, hi, ok, base, cap;
+  npr_flow *dense, *out;
+  npr_flow_v6 *dense6, *out6;
+  uint8_t *st;
+  int phase;
+} or_mt_job;
+
+static void *or_mt_run(void *arg) {
+  or_mt_job *j = (or_mt_job *)arg;
+  if (j->phase == 0) {
+    j->ok = 0;
+    for (size_t i = j->lo; i < j->hi; ++i) {
+      j->st[i] = (uint8_t)record_flow(j->in, j->len, &j->recs[i], &j->dense[i], &j->dense6[i]);
+      j->ok += j->st[i] == NPR_FLOW_OK;
+    }
+  } else {
+    size_t k = j->base; /* Ok flows of the records after this range come first */
+    for (size_t i = j->hi; i-- > j->lo;) {
+      if (j->st[i] != NPR_FLOW_OK) continue;
+      if (k < j->cap) {
+        j->out[k] = j->dense[i];
+        if (j->out6) j->out6[k] = j->dense6[i];
+      }
+      k++;
+    }
+  }
+  return NULL;
+}
+
+size_t or_bench_extract_mt(const uint8_t *in, size_t len, npr_record *rec_scratch, size_t rec_cap,
+                           npr_flow *dense, npr_flow_v6 *dense6, uint8_t *status, npr_flow *out,
+                           npr_flow_v6 *out6, size_t flow_cap, size_t *n_records, int nthreads) {
+  npr_global_header h;
+  size_t n = 0, cons = 0;
+  if (or_capture_file_parse(in, len, &h, rec_scratch, rec_cap, &n, &cons) != OR_OK) {
+    if (n_records) *n_records = 0;
+    return 0;
+  }
+  if (n_records) *n_records = n;
+  if (n > rec_cap) n = rec_cap;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  or_mt_job jobs[256];
+  pthread_t th[256];
+  for (int t = 0; t < nthreads; ++t) {
+    or_mt_job *j = &jobs[t];
+    j->in = in, j->len = len, j->recs = rec_scratch;
+    j->lo = n * (size_t)t / (size_t)nthreads, j->hi = n * (size_t)(t + 1) / (size_t)nthreads;
+    j->dense = dense, j->dense6 = dense6, j->st = status, j->out = out, j->out6 = out6, j->cap = flow_cap;
+    j->phase = 0;
+  }
+  for (int ph = 0; ph < 2; ++ph) {
+    if (ph == 1) { /* exclusive prefix from the END: the last range's flows are rows 0.. */
+      size_t acc = 0;
+      for (int t = nthreads; t-- > 0;) {
+        jobs[t].base = acc;
+        acc += jobs[t].ok;
+        jobs[t].phase = 1;
+      }
+    }
+    for (int t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, or_mt_run, &jobs[t]);
+    or_mt_run(&jobs[0]);
+    for (int t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+  }
+  size_t total = 0;
+  for (int t = 0; t < nthreads; ++t) total += jobs[t].ok;
+  return total;
+}

@@ -90,6 +90,12 @@ size_t or_bench_extract(const uint8_t *in, size_t len, npr_record *rec_scratch, 
                         npr_flow *flow_scratch, npr_flow_v6 *v6_scratch, size_t flow_cap,
                         size_t *n_records);
 
+/* The same on `nthreads` host threads (serial chain walk, parallel extract_flow, reverse-order
+ * rows from per-thread Ok counts).  dense / dense6 / status: n-record scratch. */
+size_t or_bench_extract_mt(const uint8_t *in, size_t len, npr_record *rec_scratch, size_t rec_cap,
+                           npr_flow *dense, npr_flow_v6 *dense6, uint8_t *status, npr_flow *out,
+                           npr_flow_v6 *out6, size_t flow_cap, size_t *n_records, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,8 @@ def lib():
         L.or_extract_flows.restype = None
         L.or_bench_extract.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _sz, _szp]
         L.or_bench_extract.restype = _sz
+        L.or_bench_extract_mt.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _sz, _szp, ctypes.c_int]
+        L.or_bench_extract_mt.restype = _sz
         L.or_eth_parse.argtypes = [_vp, _sz, ctypes.POINTER(OrEth)]
         L.or_ipv4_parse.argtypes = [_vp, _sz, ctypes.POINTER(OrIp)]
         L.or_ipv6_parse.argtypes = [_vp, _sz, ctypes.POINTER(OrIp)]
@@ -157,4 +159,28 @@ def bench_extract(data, rec_scratch, flow_scratch, v6_scratch):
     k = lib().or_bench_extract(p, a.size, rec_scratch.ctypes.data, rec_scratch.size,
                                flow_scratch.ctypes.data, v6_scratch.ctypes.data, flow_scratch.size,
                                ctypes.byref(nrec))
+    return k, nrec.value
+
+
+class MtScratch:
+    """Scratch of the multi-threaded bench leg for captures of up to n records."""
+
+    def __init__(self, n):
+        n = max(n, 1)
+        self.rec = np.zeros(n, dtype=_abi.RECORD_DTYPE)
+        self.dense = np.zeros(n, dtype=_abi.FLOW_DTYPE)
+        self.dense6 = np.zeros(n, dtype=_abi.FLOW_V6_DTYPE)
+        self.status = np.zeros(n, dtype=np.uint8)
+        self.out = np.zeros(n, dtype=_abi.FLOW_DTYPE)
+        self.out6 = np.zeros(n, dtype=_abi.FLOW_V6_DTYPE)
+
+
+def bench_extract_mt(data, scratch, nthreads):
+    """bench_extract on `nthreads` host threads; returns (n_flows, n_records); flows in scratch.out."""
+    a, p = _buf(data)
+    nrec = _sz(0)
+    s = scratch
+    k = lib().or_bench_extract_mt(p, a.size, s.rec.ctypes.data, s.rec.size, s.dense.ctypes.data, s.dense6.ctypes.data,
+                                  s.status.ctypes.data, s.out.ctypes.data, s.out6.ctypes.data, s.out.size,
+                                  ctypes.byref(nrec), int(nthreads))
     return k, nrec.value

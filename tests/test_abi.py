@@ -39,13 +39,14 @@ def test_library_is_gfx950_code_object():
 
 
 def test_struct_sizes_match_c():
+    import ctypes
     code = r'''
 #include <stdio.h>
 #include <stddef.h>
 #include "npr.h"
-int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_header), sizeof(npr_record),
+int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_header), sizeof(npr_record),
  sizeof(npr_flow), sizeof(npr_flow_v6), sizeof(npr_summary), sizeof(npr_dev_outputs),
- offsetof(npr_flow, kind), offsetof(npr_flow, record_offset)); return 0;}'''
+ offsetof(npr_flow, kind), offsetof(npr_flow, record_offset), sizeof(npr_shard)); return 0;}'''
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "t.c")
@@ -54,14 +55,13 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global_hea
                        check=True)
         vals = list(map(int, subprocess.run([os.path.join(d, "t")], capture_output=True, text=True).stdout.split()))
     assert vals == [24, 24, 32, 32, 40, 64, _abi.FLOW_DTYPE.fields["kind"][1],
-                    _abi.FLOW_DTYPE.fields["record_offset"][1]]
-    import ctypes
+                    _abi.FLOW_DTYPE.fields["record_offset"][1], ctypes.sizeof(_abi.ShardC)]
     assert ctypes.sizeof(_abi.DevOutputsC) == 64
 
 
 def test_abi_version():
     lib = _abi.load_library()
-    assert lib.npr_abi_version() == 2
+    assert lib.npr_abi_version() == 3
     assert b"gfx950" in lib.npr_version()
 
 

@@ -66,8 +66,10 @@ def test_sharded_device_matches_serial(world, corpus):
     results, live, rounds = parallel.parse_sharded_inprocess(local, 24, len(blob), world)
     _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
     assert r_tot == len(recs) and f_tot == len(flows)
-    merged = parallel.merge_flows(results, live)
+    merged, merged6 = parallel.merge_flows(results, live)
     assert merged.tobytes() == flows.tobytes()
+    m = (flows["kind"] & _abi.KIND_IPV6) != 0
+    assert merged6[m].tobytes() == v6[m].tobytes()
     last = [r for r in range(world) if live[r]][-1]
     assert results[last].consumed == cons or results[last].consumed >= len(blob)
 
@@ -80,4 +82,4 @@ def test_sharded_device_chain_end():
     results, live, rounds = parallel.parse_sharded_inprocess(local, 24, len(blob), 4)
     _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
     assert r_tot == 9_000 and f_tot == len(flows)
-    assert parallel.merge_flows(results, live).tobytes() == flows.tobytes()
+    assert parallel.merge_flows(results, live)[0].tobytes() == flows.tobytes()

@@ -1,0 +1,190 @@
+"""Parity at the BASELINE.json configurations' full sizes, on one GPU (SURVEY.md §8 rows a–e):
+
+- C2: the exact bench launch (1M x 64-B records, one resident launch, flows-only workspace) is
+  byte-compared with the oracle;
+- C3: the full 8M-record variable-length capture (6.4 GB, chained resident launches) is
+  byte-compared with the oracle;
+- C4: the 64M-record capture sharded by record range into 8 shards, each shard in its OWN HBM
+  buffer holding only its file bytes (npr_dev_parse_extract_shard, exactly what each rank of the
+  8-GPU run holds), reconciled by the one-exchange replay and merged in reverse rank order: bit-exact
+  against the oracle at 16M records, and at the full 64M;
+- C5 substitute (the 4SICS capture is absent, .MISSING_LARGE_BLOBS:1): a quirk-corpus tile
+  repeated to several GB, sharded by BYTE range with halos (speculated starts inside adversarial
+  payloads), every tile of the merged table compared with the single-tile oracle golden.
+
+The oracle (tests/_oracle.py) is the checker only.  Heavy cases print progress so a long run is
+never silent."""
+import time
+
+import numpy as np
+import pytest
+import torch
+
+import _oracle
+from net_parser_rs import _abi, device, parallel, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def log(msg):
+    print(f"[{time.strftime('%H:%M:%S')}] {msg}", flush=True)
+
+
+def to_dev(a):
+    a = np.frombuffer(a, dtype=np.uint8) if isinstance(a, (bytes, bytearray)) else a
+    t = torch.empty(a.size, dtype=torch.uint8, device="cuda")
+    t.copy_(torch.from_numpy(a))
+    return t
+
+
+def oracle_flows(blob):
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    assert rc == 0
+    flows, v6 = _oracle.convert_records(blob, recs)
+    return hdr, recs, cons, flows, v6
+
+
+def v6_rows(flows, v6):
+    m = (flows["kind"] & _abi.KIND_IPV6) != 0
+    return v6[m]
+
+
+def test_c2_bench_launch_bit_exact():
+    """The exact launch bench.py times: 1M records, one k_parse_resident dispatch."""
+    blob = synth.fixed64(1_000_000)
+    hdr, recs, cons, flows, _ = oracle_flows(blob)
+    n = len(recs)
+    ws = device.Workspace(record_cap=n, flow_cap=n, records=False, offsets=False, status=False,
+                          flows=True, flows_v6=True)
+    ws.launch(to_dev(blob), start=24, endianness=hdr.endianness)
+    sm = ws.check()
+    assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons)
+    assert ws.flows_np().tobytes() == flows.tobytes()
+
+
+def test_c3_full_8m_bit_exact():
+    log("C3: generating 8M variable-length records")
+    blob = synth.variable_mix(8_000_000)
+    log(f"C3: {len(blob)} B; oracle")
+    hdr, recs, cons, flows, _ = oracle_flows(blob)
+    n = len(recs)
+    assert n == 8_000_000
+    log("C3: device")
+    ws = device.Workspace(record_cap=n, flow_cap=n, records=False, offsets=False, status=False,
+                          flows=True, flows_v6=True)
+    buf = to_dev(blob)
+    ws.launch(buf, start=24, endianness=hdr.endianness)  # chained resident launches
+    sm = ws.check()
+    assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons)
+    got = ws.flows_np()
+    assert got.tobytes() == flows.tobytes()
+    log("C3: ok")
+
+
+def c4_shards(n_records, world, host=None):
+    """Each rank's buffer exactly as the 8-GPU run lays it out: its own file bytes only."""
+    layout = parallel.record_range_shards(n_records, world)
+    bufs = []
+    for g, (base, start, stop, spec) in enumerate(layout):
+        r0, r1 = n_records * g // world, n_records * (g + 1) // world
+        a = synth.fixed64_range(r0, r1) if host is None else host[base:stop]
+        assert a.size == stop - base
+        bufs.append(to_dev(np.ascontiguousarray(a)))
+    return layout, bufs
+
+
+def run_c4(n_records, world=8):
+    log(f"C4 {n_records}: generating")
+    host = synth.fixed64_range(0, n_records)
+    file_len = host.size
+    layout, bufs = c4_shards(n_records, world, host)
+    per = n_records // world + 1
+    locals_ = []
+    for (base, start, stop, spec), b in zip(layout, bufs):
+        ws = device.Workspace(record_cap=1, flow_cap=per, records=False, offsets=False, status=False,
+                              flows=True, flows_v6=True)
+        locals_.append(parallel.shard_local(ws, b, base, file_len, usec_magic=True, ts_ref=1_600_000_000,
+                                            to_host=True))
+    bounds = [(start if g == 0 else base, stop) for g, (base, start, stop, spec) in enumerate(layout)]
+    bounds[0] = (24, layout[0][2])
+    log("C4: device shards")
+    results, live, rounds = parallel.parse_sharded_inprocess(locals_, 24, file_len, world, bounds=bounds)
+    assert rounds == 1 and all(live)
+    for g, r in enumerate(results):  # every speculated start was the exact record boundary
+        assert r.entry == bounds[g][0] and r.consumed == bounds[g][1]
+    merged, merged6 = parallel.merge_flows(results, live)
+    log("C4: oracle")
+    hdr, recs, cons, flows, v6 = oracle_flows(host)
+    assert len(recs) == n_records and cons == file_len
+    _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
+    assert (r_tot, f_tot) == (n_records, len(flows))
+    assert merged.tobytes() == flows.tobytes()
+    log("C4: ok")
+
+
+def test_c4_16m_sharded_bit_exact():
+    run_c4(16_000_000)
+
+
+def test_c4_64m_sharded_bit_exact():
+    run_c4(64_000_000)
+
+
+def test_c5_tiled_quirk_capture():
+    """SURVEY.md §8 d C5 with the quirk corpus standing in for the absent 4SICS file: one tile of
+    complete records repeated to ~4 GB; byte-range shards with halos; each tile's slice of the
+    merged table equals the single-tile golden with its record offsets moved by the tile's place."""
+    tile_blob = synth.quirk_corpus(30_000, seed=77, fake_every=25, jumbo_every=5_000)
+    hdr, recs, cons, gold, gold6 = oracle_flows(tile_blob)
+    assert cons == len(tile_blob)       # a tile of complete records: the chain runs on into the next
+    body = np.frombuffer(tile_blob, dtype=np.uint8)[24:]
+    T, K = body.size, 4_000_000_000 // body.size
+    log(f"C5: tile {T} B x {K}")
+    host = np.empty(24 + T * K, dtype=np.uint8)
+    host[:24] = np.frombuffer(tile_blob[:24], dtype=np.uint8)
+    host[24:] = np.tile(body, K)
+    file_len = host.size
+    world, halo = 8, 1 << 20             # jumbo records are <= 70 KB: a 1 MiB halo holds any record
+    bounds = parallel.shard_bounds(24, file_len, world)
+    locals_ = []
+    for g, (lo, hi) in enumerate(bounds):
+        base = 0 if g == 0 else lo - lo % 16
+        end = min(file_len, hi + halo)
+        ws = device.Workspace(record_cap=1, flow_cap=len(gold) * (K // world + 2), records=False, offsets=False,
+                              status=False, flows=True, flows_v6=True)
+        locals_.append(parallel.shard_local(ws, to_dev(np.ascontiguousarray(host[base:end])), base, file_len,
+                                            usec_magic=True, ts_ref=1_600_000_000, to_host=True))
+    log("C5: device shards")
+    results, live, rounds = parallel.parse_sharded_inprocess(locals_, 24, file_len, world, bounds=bounds)
+    merged, merged6 = parallel.merge_flows(results, live)
+    n = len(gold)
+    assert all(live) and len(merged) == n * K
+    # tile k occupies rows [(K-1-k) * n, (K-k) * n) of the reverse-order table
+    got = merged.reshape(K, n)[::-1]
+    off = got["record_offset"].astype(np.uint64)
+    goff = gold["record_offset"].astype(np.uint64)
+    offs = sum(off[..., i] << np.uint64(8 * i) for i in range(5))
+    goffs = sum(goff[..., i] << np.uint64(8 * i) for i in range(5))
+    want = goffs[None, :] + np.arange(K, dtype=np.uint64)[:, None] * np.uint64(T)
+    assert np.array_equal(offs, want)
+    strip = lambda a: a.view(np.uint8).reshape(a.shape + (32,))[..., :27]  # every field but the offset
+    assert np.array_equal(strip(got), np.broadcast_to(strip(gold), got.shape + (27,)))
+    g6 = merged6.reshape(K, n)[::-1]
+    m = (gold["kind"] & _abi.KIND_IPV6) != 0
+    assert m.any() and np.array_equal(g6[:, m], np.broadcast_to(gold6[m], (K, int(m.sum()))))
+    log(f"C5: ok ({rounds} exchange rounds)")
+
+
+@pytest.mark.parametrize("records", [3_100, 50_000, 250_000])
+def test_fresh_context_slot_sizing(records):
+    """Resident launches of 61, ~1000 and ~4900 tiles on FRESH contexts (the workgroup
+    aggregates once overran the slot allocation at these sizes; the host now refuses such a launch)."""
+    import net_parser_rs as npr
+    blob = synth.fixed64(records)
+    hdr, recs, cons, flows, _ = oracle_flows(blob)
+    ws = device.Workspace(record_cap=1, flow_cap=len(recs), records=False, flows=True, flows_v6=False,
+                          ctx=npr.Context(0))
+    ws.launch(to_dev(blob), start=24, endianness=hdr.endianness)
+    sm = ws.check()
+    assert (sm.n_records, sm.consumed) == (len(recs), cons)
+    assert ws.flows_np().tobytes() == flows.tobytes()

@@ -14,11 +14,11 @@ import _oracle
 from net_parser_rs import _abi, parallel, synth
 
 
-def full_reference(blob):
+def full_reference(blob, with_v6=False):
     rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
     assert rc == 0
     flows, v6 = _oracle.convert_records(blob, recs)
-    return hdr, recs, cons, flows
+    return (hdr, recs, cons, flows, v6) if with_v6 else (hdr, recs, cons, flows)
 
 
 def oracle_local(blob, endianness, spec):
@@ -28,14 +28,15 @@ def oracle_local(blob, endianness, spec):
         if speculative:
             start = spec(lo, hi)
             if start is None:
-                return parallel.ShardResult(_abi.NO_ENTRY, hi, 0, 0, np.zeros(0, _abi.FLOW_DTYPE))
+                return parallel.ShardResult(_abi.NO_ENTRY, hi, 0, 0, np.zeros(0, _abi.FLOW_DTYPE),
+                                            np.zeros(0, _abi.FLOW_V6_DTYPE))
         recs, cons = _oracle.records_parse(blob[start:], endianness)
         recs = recs.copy()
         recs["offset"] += start
         keep = recs[recs["offset"] < hi]
         consumed = int(recs["offset"][len(keep)]) if len(keep) < len(recs) else start + cons
-        flows, _ = _oracle.convert_records(blob, keep)
-        return parallel.ShardResult(start, consumed, len(keep), len(flows), flows)
+        flows, v6 = _oracle.convert_records(blob, keep)
+        return parallel.ShardResult(start, consumed, len(keep), len(flows), flows, v6)
     return local
 
 
@@ -59,14 +60,21 @@ def spec_off_by(recs, skip):
     return spec
 
 
+def v6_rows(flows, v6):
+    """The IPv6 side rows that carry data (rows of IPv4 flows are unspecified)."""
+    m = (flows["kind"] & _abi.KIND_IPV6) != 0
+    return v6[m].tobytes()
+
+
 def check_merge(blob, world, spec_maker):
-    hdr, recs, cons, flows = full_reference(blob)
+    hdr, recs, cons, flows, v6 = full_reference(blob, with_v6=True)
     local = oracle_local(blob, hdr.endianness, spec_maker(recs))
     results, live, rounds = parallel.parse_sharded_inprocess(local, 24, len(blob), world)
-    merged = parallel.merge_flows(results, live)
+    merged, merged6 = parallel.merge_flows(results, live)
     _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
     assert r_tot == len(recs) and f_tot == len(flows)
     assert merged.tobytes() == flows.tobytes()
+    assert v6_rows(merged, merged6) == v6_rows(flows, v6)
     return rounds
 
 
@@ -123,14 +131,19 @@ def _rank_main(rank, world, port, blob, wrong, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        hdr, recs, cons, flows = full_reference(blob)
+        hdr, recs, cons, flows, v6 = full_reference(blob, with_v6=True)
         spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
         local = oracle_local(blob, hdr.endianness, spec)
         mine, metas, live, rounds = parallel.parse_sharded(local, 24, len(blob))
-        merged = parallel.gather_flows(mine, metas, live)
+        got = parallel.gather_flows(mine, metas, live)
         if rank == 0:
+            merged, merged6 = got
             _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
-            q.put((r_tot == len(recs), f_tot == len(flows), merged.tobytes() == flows.tobytes(), rounds))
+            n6 = int(((flows["kind"] & _abi.KIND_IPV6) != 0).sum())
+            q.put((r_tot == len(recs), f_tot == len(flows), merged.tobytes() == flows.tobytes(),
+                   n6 > 0 and v6_rows(merged, merged6) == v6_rows(flows, v6), rounds))
+        else:
+            assert got is None
     finally:
         dist.destroy_process_group()
 
@@ -147,6 +160,100 @@ def test_gloo_world2(wrong):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    recs_ok, flows_ok, bytes_ok, rounds = q.get(timeout=10)
-    assert recs_ok and flows_ok and bytes_ok
+    recs_ok, flows_ok, bytes_ok, v6_ok, rounds = q.get(timeout=10)
+    assert recs_ok and flows_ok and bytes_ok and v6_ok
+    assert (rounds > 1) == wrong
+
+
+# ---- the device step's exchange protocol (DeviceShardedParse) over gloo ------------------------
+class OracleShardWorkspace:
+    """Stands in for device.Workspace on CPU: npr_dev_parse_extract_shard's contract (records that
+    start in [start, stop), flow rows right-aligned, the summary as the device writes it), computed
+    by the oracle from the rank's OWN shard bytes only (file offsets)."""
+
+    def __init__(self, flow_cap, spec):
+        import torch
+        self.flow_cap, self.spec = flow_cap, spec
+        self.summary = torch.zeros(64, dtype=torch.uint8)
+        self.flows = torch.zeros(flow_cap * 32, dtype=torch.uint8)
+        self.flows_v6 = torch.zeros(flow_cap * 32, dtype=torch.uint8)
+
+    def launch_shard(self, buf, base, start, stop, endianness=0, speculative=False, usec_magic=True, ts_ref=None,
+                     chunk_bytes=0, nbytes=None):
+        import torch
+        shard = buf.numpy().tobytes()
+        if speculative:
+            start = self.spec(start, stop)
+        if start is None:
+            sm = (0, 0, stop, _abi.NO_ENTRY)
+            n_flows = 0
+        else:
+            recs, cons = _oracle.records_parse(shard[start - base:], endianness)
+            recs = recs.copy()
+            recs["offset"] += start - base
+            keep = recs[recs["offset"] + base < stop]
+            consumed = int(recs["offset"][len(keep)]) + base if len(keep) < len(recs) else start + cons
+            flows, v6 = _oracle.convert_records(shard, keep)
+            off = flows["record_offset"].astype(np.uint64)
+            o = sum(off[:, i] << np.uint64(8 * i) for i in range(5)) + np.uint64(base)  # file offsets
+            for i in range(5):
+                flows["record_offset"][:, i] = ((o >> np.uint64(8 * i)) & np.uint64(0xff)).astype(np.uint8)
+            n_flows = len(flows)
+            self.flows[(self.flow_cap - n_flows) * 32:] = torch.from_numpy(flows.view(np.uint8).reshape(-1).copy())
+            self.flows_v6[(self.flow_cap - n_flows) * 32:] = torch.from_numpy(v6.view(np.uint8).reshape(-1).copy())
+            sm = (len(keep), n_flows, consumed, start)
+        s = np.zeros(1, dtype=_abi.SUMMARY_DTYPE)
+        s["n_records"], s["n_flows"], s["consumed"], s["entry"] = sm
+        s["epoch"], s["flags"] = 1, 0
+        self.summary[:40] = torch.from_numpy(s.view(np.uint8).copy())
+
+    def flow_rows(self, n):
+        lo = (self.flow_cap - n) * 32
+        return self.flows[lo:], self.flows_v6[lo:]
+
+
+def _step_rank_main(rank, world, port, blob, wrong, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hdr, recs, cons, flows, v6 = full_reference(blob, with_v6=True)
+        bounds = parallel.shard_bounds(24, len(blob), world)
+        lo, hi = bounds[rank]
+        base = 0 if rank == 0 else lo - lo % 16
+        end = min(len(blob), hi + (1 << 20))
+        shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
+        spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
+        ws = OracleShardWorkspace(len(recs) + 1, spec)
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
+        metas, live, rounds = step.step()
+        fl, f6 = step.rows()
+        merged, merged6 = parallel.gather_flow_tables(fl, f6, metas, live)
+        if rank == 0:
+            m = merged.numpy().view(_abi.FLOW_DTYPE)
+            m6 = merged6.numpy().view(_abi.FLOW_V6_DTYPE)
+            q.put((m.tobytes() == flows.tobytes(), v6_rows(m, m6) == v6_rows(flows, v6), rounds))
+        else:
+            assert merged is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("wrong", [False, True], ids=["exact", "rerun"])
+def test_gloo_world2_device_step_protocol(wrong):
+    """DeviceShardedParse (the bench's multi-GPU step) + gather_flow_tables over gloo: each rank holds
+    only its shard's bytes; summaries all-gathered, the chain replayed, a wrong speculated start
+    re-parsed, flow rows sent point-to-point into the root's merged table."""
+    blob = synth.quirk_corpus(2_500, seed=36)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_step_rank_main, args=(r, 2, port, blob, wrong, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    flows_ok, v6_ok, rounds = q.get(timeout=10)
+    assert flows_ok and v6_ok
     assert (rounds > 1) == wrong
