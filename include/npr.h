@@ -253,6 +253,25 @@ npr_status npr_parse_extract(npr_ctx *ctx, const uint8_t *input, size_t len,
                              size_t *n_records, npr_flow *out, npr_flow_v6 *out_v6,
                              size_t flow_cap, size_t *n_flows, size_t *consumed);
 
+/* The same `extract` step with the PCIe transfers pipelined (row f1; the north star's end-to-end
+ * path): the capture goes to the device in chunks of `chunk_bytes` (0 = 32 MiB) by page-locked
+ * DMA on one stream; each chunk's chained parse launches as soon as it (and the next chunk, for
+ * records that straddle) has landed; each launch's flow rows go back on a third stream while
+ * later chunks still upload (PCIe is full duplex).  Caller buffers that are not page-locked
+ * (npr_host_alloc, or registered by the caller) are registered for the call.  The flows land
+ * RIGHT-aligned, the device table's own layout: out[flow_cap - *n_flows .. flow_cap) in
+ * convert_records order, so no pass moves them afterwards.  A record longer than a chunk ends a
+ * link early; the call detects that and parses the staged capture again in one go.  Results
+ * equal npr_parse_extract's. */
+npr_status npr_parse_extract_pipelined(npr_ctx *ctx, const uint8_t *input, size_t len,
+                                       npr_global_header *header, npr_flow *out, npr_flow_v6 *out_v6,
+                                       size_t flow_cap, size_t *n_flows, size_t *consumed,
+                                       uint64_t chunk_bytes);
+/* Page-locked host memory for captures and flow tables (hipHostMalloc): the DMA engines read and
+ * write it at full PCIe rate, with no per-call registration. */
+npr_status npr_host_alloc(npr_ctx *ctx, size_t bytes, void **out);
+npr_status npr_host_free(npr_ctx *ctx, void *p);
+
 /* ---- device-resident entry points ------------------------------------------------------- */
 /* The hot path: one launch finds the record chain starting at `start` (24 for a capture
  * file, 0 for bare records), decodes every record and writes the outputs described in

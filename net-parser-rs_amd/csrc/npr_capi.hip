@@ -50,6 +50,11 @@ struct npr_ctx {
   uint64_t stream_chunk = 0;  // NPR_OPT_STREAM_CHUNK (KiB in the option; 0 = one copy, the default)
   hipStream_t copy_stream = nullptr;
   std::vector<hipEvent_t> copied;       // one per chunk in flight
+  // npr_parse_extract_pipelined: D2H of each link's flow rows, the per-link summaries on the host
+  hipStream_t d2h_stream = nullptr;
+  std::vector<hipEvent_t> linked;
+  npr_summary *sum_host = nullptr;
+  uint64_t sum_host_cap = 0;
   std::string err;
 };
 
@@ -192,8 +197,12 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (c->summary_h) (void)hipHostFree(c->summary_h);
   if (c->stats) (void)hipFree(c->stats);
   if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
+  if (c->d2h_stream) (void)hipStreamSynchronize(c->d2h_stream);
   for (hipEvent_t ev : c->copied) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : c->linked) (void)hipEventDestroy(ev);
+  if (c->sum_host) (void)hipHostFree(c->sum_host);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+  if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -467,9 +476,16 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     if (!resident) return fail(c, NPR_ERR_ARG, "a chained launch produces flows only (resident pass)");
     if (speculative_start) return fail(c, NPR_ERR_ARG, "a chained launch continues an exact chain");
     p.prev = prev;
-    p.prev_epoch = 0;  // the epoch of the launch that wrote *prev, when it was one of ours
-    for (int i = 0; i < 2; ++i)
-      if (c->sum_ptr[i] == prev) p.prev_epoch = c->sum_epoch[i];
+    p.prev_epoch = 0;  // the epoch of the launch that wrote *prev, when it was one of ours: the
+    // most recent of the last two launches that wrote that address (an older launch may have
+    // used the same summary slot)
+    for (uint32_t k = 0; k < 2; ++k) {
+      const uint32_t i = c->sum_next ^ 1u ^ k;
+      if (c->sum_ptr[i] == prev) {
+        p.prev_epoch = c->sum_epoch[i];
+        break;
+      }
+    }
   }
   if (resident) {
     if ((st = res_geometry(c))) return st;
@@ -567,6 +583,183 @@ static npr_status stream_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64
     if (hi == len) break;
     prev = oc.summary;
   }
+  return NPR_OK;
+}
+
+// ---- pinned, overlapped host path (row f1): H2D chunks | chained launches | D2H of each link's rows
+static npr_status grow_events(npr_ctx *c, std::vector<hipEvent_t> &v, uint64_t n) {
+  while (v.size() < n) {
+    hipEvent_t ev;
+    HIP_CHECK(c, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    v.push_back(ev);
+  }
+  return NPR_OK;
+}
+
+// Is [p, p + n) page-locked host memory (hipHostMalloc'ed or registered)?
+static bool host_pinned(const void *p, size_t n) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  (void)n;
+  return a.type == hipMemoryTypeHost && a.hostPointer != nullptr;
+}
+
+npr_status npr_parse_extract_pipelined(npr_ctx *c, const uint8_t *in, size_t len, npr_global_header *hdr,
+                                       npr_flow *out, npr_flow_v6 *out_v6, size_t flow_cap, size_t *n_flows,
+                                       size_t *consumed, uint64_t chunk_bytes) {
+  if (!c || !hdr || !out || (!in && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  npr_status st = npr_global_header_parse(in, len, hdr, nullptr);  // file.rs:18
+  if (st) return st;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  const uint64_t start = 24;
+  const npr_endianness e = (npr_endianness)hdr->endianness;
+  const uint64_t chunk = std::max<uint64_t>(chunk_bytes ? chunk_bytes : (32ull << 20), 1ull << 16);
+  const uint64_t nlinks = (len + chunk - 1) / chunk;
+  const uint64_t max_rec = (len - start) / 16 + 1;
+  const uint64_t fcap = std::min<uint64_t>(flow_cap, max_rec);
+  // device row r is the caller's row r + shift: the flows end at out[flow_cap - 1]
+  const uint64_t shift = flow_cap - fcap;
+  npr_flow *hout = out + shift;
+  npr_flow_v6 *hout6 = out_v6 ? out_v6 + shift : nullptr;
+  // the caller's buffers: page-locked for the DMA engines (registered for this call unless they are)
+  struct Unreg {  // unregister on every exit path
+    void *p[3] = {nullptr, nullptr, nullptr};
+    ~Unreg() {
+      for (void *q : p)
+        if (q) (void)hipHostUnregister(q);
+    }
+  } unreg;
+  const void *bufs[3] = {in, hout, hout6};
+  const size_t sizes[3] = {len, fcap * sizeof(npr_flow), hout6 ? fcap * sizeof(npr_flow_v6) : 0};
+  for (int i = 0; i < 3; ++i) {
+    if (!sizes[i] || host_pinned(bufs[i], sizes[i])) continue;
+    const hipError_t r = hipHostRegister((void *)bufs[i], sizes[i], hipHostRegisterDefault);
+    if (r == hipErrorHostMemoryAlreadyRegistered) {
+      (void)hipGetLastError();
+      continue;
+    }
+    HIP_CHECK(c, r);
+    unreg.p[i] = (void *)bufs[i];
+  }
+  if ((st = ensure(c, c->in, len + 16))) return st;
+  if ((st = ensure(c, c->flows, std::max<uint64_t>(fcap, 1) * sizeof(npr_flow)))) return st;
+  if (out_v6 && (st = ensure(c, c->flows_v6, std::max<uint64_t>(fcap, 1) * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->chain, std::max<uint64_t>(nlinks, 2) * sizeof(npr_summary), true))) return st;
+  if (c->sum_host_cap < nlinks) {
+    if (c->sum_host) HIP_CHECK(c, hipHostFree(c->sum_host));
+    c->sum_host = nullptr;
+    c->sum_host_cap = 0;
+    HIP_CHECK(c, hipHostMalloc((void **)&c->sum_host, nlinks * sizeof(npr_summary), 0));
+    c->sum_host_cap = nlinks;
+  }
+  if (!c->copy_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  if (!c->d2h_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+  if ((st = grow_events(c, c->copied, nlinks))) return st;
+  if ((st = grow_events(c, c->linked, nlinks))) return st;
+  uint8_t *dev = (uint8_t *)c->in.p;
+  npr_summary *dsum = (npr_summary *)c->chain.p;
+  // the compute stream's earlier work (a previous parse reading the staging buffer) comes first
+  HIP_CHECK(c, hipEventRecord(c->copied[0], c->stream));
+  HIP_CHECK(c, hipStreamWaitEvent(c->copy_stream, c->copied[0], 0));
+  HIP_CHECK(c, hipStreamWaitEvent(c->d2h_stream, c->copied[0], 0));
+  HIP_CHECK(c, hipMemsetAsync(dsum, 0, nlinks * sizeof(npr_summary), c->stream));  // no stale summaries
+  for (uint64_t j = 0; j < nlinks; ++j) {  // every H2D chunk queued up front
+    const uint64_t a = j * chunk, b = std::min<uint64_t>(len, a + chunk);
+    HIP_CHECK(c, hipMemcpyAsync(dev + a, in + a, b - a, hipMemcpyHostToDevice, c->copy_stream));
+    HIP_CHECK(c, hipEventRecord(c->copied[j], c->copy_stream));
+  }
+  npr_dev_outputs o{};
+  o.flows = fcap ? (npr_flow *)c->flows.p : nullptr;
+  o.flows_v6 = (fcap && out_v6) ? (npr_flow_v6 *)c->flows_v6.p : nullptr;
+  o.flow_cap = fcap;
+  const npr_summary *prev = nullptr;
+  uint64_t last = 0;
+  for (uint64_t j = 0; j < nlinks; ++j) {  // link j: records starting in chunk j, once j and j+1 landed
+    const uint64_t lo = std::max<uint64_t>(start, j * chunk), hi = std::min<uint64_t>(len, (j + 1) * chunk);
+    const uint64_t jn = std::min<uint64_t>(j + 1, nlinks - 1);
+    HIP_CHECK(c, hipStreamWaitEvent(c->stream, c->copied[jn], 0));
+    const uint64_t readable = std::min<uint64_t>(len, (jn + 1) * chunk);
+    o.summary = dsum + j;
+    if (hi > lo || hi == len) {
+      if ((st = launch_range(c, dev, readable, std::min(lo, hi), hi, e, 0, start, prev, &o, c->stream))) return st;
+      prev = o.summary;
+    } else {  // the header alone spans this chunk: carry the previous summary (nothing starts here)
+      HIP_CHECK(c, hipMemsetAsync(o.summary, 0, sizeof(npr_summary), c->stream));
+    }
+    HIP_CHECK(c, hipMemcpyAsync(c->sum_host + j, prev ? prev : o.summary, sizeof(npr_summary), hipMemcpyDeviceToHost,
+                                c->stream));
+    HIP_CHECK(c, hipEventRecord(c->linked[j], c->stream));
+    last = j;
+  }
+  // the flow rows of each link go back as soon as it is done, while later chunks still upload:
+  // link j's rows are [fcap - cum_j, fcap - cum_{j-1}) of the right-aligned table (cum = running
+  // n_flows), the same rows of the caller's table
+  uint64_t cum = 0;
+  npr_summary fin{};
+  for (uint64_t j = 0; j <= last; ++j) {
+    HIP_CHECK(c, hipEventSynchronize(c->linked[j]));
+    const npr_summary sj = c->sum_host[j];
+    if (sj.epoch == 0) continue;  // nothing launched yet (a header spanning the first chunk)
+    fin = sj;
+    const uint64_t nc = std::min<uint64_t>(sj.n_flows, fcap);
+    if (nc > cum) {
+      HIP_CHECK(c, hipStreamWaitEvent(c->d2h_stream, c->linked[j], 0));
+      HIP_CHECK(c, hipMemcpyAsync(hout + (fcap - nc), (npr_flow *)c->flows.p + (fcap - nc), (nc - cum) * sizeof(npr_flow),
+                                  hipMemcpyDeviceToHost, c->d2h_stream));
+      if (hout6)
+        HIP_CHECK(c, hipMemcpyAsync(hout6 + (fcap - nc), (npr_flow_v6 *)c->flows_v6.p + (fcap - nc),
+                                    (nc - cum) * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->d2h_stream));
+      cum = nc;
+    }
+  }
+  HIP_CHECK(c, hipStreamSynchronize(c->d2h_stream));
+  if (fin.epoch != c->epoch) {  // which link stopped, and did a bounded wait abort it?
+    uint32_t ab = 0;
+    HIP_CHECK(c, hipMemcpy(&ab, c->abort_word, 4, hipMemcpyDeviceToHost));
+    uint64_t bad = 0;
+    while (bad <= last && c->sum_host[bad].epoch != 0) ++bad;
+    return fail(c, NPR_ERR_TIMEOUT,
+                "pipelined parse did not complete: link %llu of %llu wrote no summary (last epoch %u, context epoch %u, "
+                "abort word %u)",
+                (unsigned long long)bad, (unsigned long long)(last + 1), fin.epoch, c->epoch, ab);
+  }
+  if (fin.consumed + 16 <= len) {  // the chain stopped at a complete record longer than a chunk:
+    const uint64_t incl = rd_u32(in + fin.consumed + 8, e == NPR_BIG);  // parse the staged capture whole
+    if (incl <= len - fin.consumed - 16) {
+      o.summary = c->summary;
+      if ((st = npr_dev_parse_extract(c, dev, len, start, e, &o, c->stream))) return st;
+      if ((st = npr_dev_check(c, &o, c->stream, &fin)) && st != NPR_ERR_CAPACITY) return st;
+      const uint64_t nc = std::min<uint64_t>(fin.n_flows, fcap);
+      if (nc) {
+        HIP_CHECK(c, hipMemcpyAsync(hout + (fcap - nc), (npr_flow *)c->flows.p + (fcap - nc), nc * sizeof(npr_flow),
+                                    hipMemcpyDeviceToHost, c->stream));
+        if (hout6)
+          HIP_CHECK(c, hipMemcpyAsync(hout6 + (fcap - nc), (npr_flow_v6 *)c->flows_v6.p + (fcap - nc),
+                                      nc * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
+        HIP_CHECK(c, hipStreamSynchronize(c->stream));
+      }
+    }
+  }
+  if (n_flows) *n_flows = fin.n_flows;
+  if (consumed) *consumed = fin.consumed;
+  if (fin.n_flows > flow_cap || fin.flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+  return NPR_OK;
+}
+
+npr_status npr_host_alloc(npr_ctx *c, size_t bytes, void **out) {
+  if (!c || !out) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  *out = nullptr;
+  HIP_CHECK(c, hipHostMalloc(out, bytes ? bytes : 1, 0));
+  return NPR_OK;
+}
+
+npr_status npr_host_free(npr_ctx *c, void *p) {
+  if (!c) return NPR_ERR_ARG;
+  if (p) HIP_CHECK(c, hipHostFree(p));
   return NPR_OK;
 }
 

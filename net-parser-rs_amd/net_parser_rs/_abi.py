@@ -94,6 +94,7 @@ EXPORTED = [
     "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps", "npr_ctx_set_option",
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
+    "npr_parse_extract_pipelined", "npr_host_alloc", "npr_host_free",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
 ]
@@ -125,6 +126,10 @@ _SIGNATURES = {
     "npr_parse_extract": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _vp,
                                          ctypes.c_size_t, _c_size_p, _vp, _vp, ctypes.c_size_t, _c_size_p,
                                          _c_size_p]),
+    "npr_parse_extract_pipelined": (ctypes.c_int, [_vp, _u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _vp, _vp,
+                                                   ctypes.c_size_t, _c_size_p, _c_size_p, ctypes.c_uint64]),
+    "npr_host_alloc": (ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    "npr_host_free": (ctypes.c_int, [_vp, _vp]),
     "npr_dev_parse_extract": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
                                              ctypes.POINTER(DevOutputsC), _vp]),
     "npr_dev_parse_extract_range": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,

@@ -170,3 +170,40 @@ def host_parse_extract(data, flow_cap=None, with_v6=True, ctx=None):
     ctx.check(st)
     k = min(n_flows.value, cap)
     return flows[:k], (v6[:k] if v6 is not None else None), n_flows.value, consumed.value, hdr
+
+
+class PinnedArray:
+    """A page-locked host buffer from npr_host_alloc, viewed as a numpy array (freed on close)."""
+
+    def __init__(self, nbytes, dtype=np.uint8, ctx=None):
+        self.ctx = ctx or context(0)
+        p = ctypes.c_void_p()
+        self.ctx.check(self.ctx.lib.npr_host_alloc(self.ctx.handle, max(int(nbytes), 1), ctypes.byref(p)))
+        self.ptr = p
+        raw = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
+        self.array = np.frombuffer(raw, dtype=np.uint8)[: int(nbytes)].view(dtype)
+
+    def close(self):
+        if self.ptr is not None:
+            self.array = None
+            self.ctx.lib.npr_host_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+
+def host_parse_extract_pipelined(data, out=None, out_v6=None, flow_cap=None, chunk_bytes=0, ctx=None):
+    """npr_parse_extract_pipelined: a host capture (numpy uint8, ideally a PinnedArray's) in, the
+    convert_records flow table out on the host, transfers overlapped.  Returns (flows, flows_v6 or
+    None, n_flows, consumed): views of the right-aligned rows of `out` / `out_v6`."""
+    a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    ctx = ctx or context(0)
+    cap = max((a.size - 24) // 16 + 1, 1) if flow_cap is None else flow_cap
+    if out is None:
+        out = np.zeros(cap, dtype=_abi.FLOW_DTYPE)
+    hdr = _abi.GlobalHeaderC()
+    n_flows, consumed = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    st = ctx.lib.npr_parse_extract_pipelined(ctx.handle, a.ctypes.data if a.size else None, a.size, ctypes.byref(hdr),
+                                             out.ctypes.data, out_v6.ctypes.data if out_v6 is not None else None, cap,
+                                             ctypes.byref(n_flows), ctypes.byref(consumed), int(chunk_bytes))
+    ctx.check(st)
+    k = min(n_flows.value, cap)
+    return out[cap - k:cap], (out_v6[cap - k:cap] if out_v6 is not None else None), n_flows.value, consumed.value

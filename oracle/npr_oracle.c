@@ -400,7 +400,7 @@ size_t or_bench_extract(const uint8_t *in, size_t len, npr_record *rec_scratch, 
 #include <pthread.h>
 
 typedef struct {
-  const uint8_t *in;
+  _Alignas(128) const uint8_t *in;
   size_t len;
   const npr_record *recs;
   size_t lo, hi, ok, base, cap;
@@ -413,11 +413,13 @@ typedef struct {
 static void *or_mt_run(void *arg) {
   or_mt_job *j = (or_mt_job *)arg;
   if (j->phase == 0) {
-    j->ok = 0;
+    size_t ok = 0; /* a local count: the jobs share cache lines */
     for (size_t i = j->lo; i < j->hi; ++i) {
-      j->st[i] = (uint8_t)record_flow(j->in, j->len, &j->recs[i], &j->dense[i], &j->dense6[i]);
-      j->ok += j->st[i] == NPR_FLOW_OK;
+      const int st = record_flow(j->in, j->len, &j->recs[i], &j->dense[i], &j->dense6[i]);
+      j->st[i] = (uint8_t)st;
+      ok += st == NPR_FLOW_OK;
     }
+    j->ok = ok;
   } else {
     size_t k = j->base; /* Ok flows of the records after this range come first */
     for (size_t i = j->hi; i-- > j->lo;) {

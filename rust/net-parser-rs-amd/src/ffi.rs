@@ -1,0 +1,131 @@
+//! `extern "C"` view of include/npr.h (ABI 3): the entry points this crate binds, with the
+//! reference functions they replace.
+#![allow(non_camel_case_types)]
+
+use std::os::raw::{c_char, c_int, c_void};
+
+pub type npr_status = c_int;
+pub const NPR_OK: npr_status = 0;
+pub const NPR_INCOMPLETE: npr_status = 1; // crate::errors::Error::Incomplete (src/errors.rs:5)
+pub const NPR_FAILURE: npr_status = 2; // Error::Failure (src/errors.rs:7)
+pub const NPR_CUSTOM: npr_status = 3; // Error::Custom (src/errors.rs:9)
+pub const NPR_ERR_CAPACITY: npr_status = -3;
+pub const NPR_LITTLE: c_int = 0;
+pub const NPR_BIG: c_int = 1;
+pub const NPR_ABI_VERSION: c_int = 3;
+pub const NPR_FLOW_KIND_IPV6: u8 = 0x1;
+pub const NPR_FLOW_KIND_UDP: u8 = 0x2;
+
+#[repr(C)]
+pub struct npr_ctx {
+    _private: [u8; 0],
+}
+
+/// GlobalHeader (src/global_header.rs:13-23)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_global_header {
+    pub endianness: i32,
+    pub version_major: u16,
+    pub version_minor: u16,
+    pub zone: i32,
+    pub sig_figs: i32,
+    pub snap_length: u32,
+    pub network: u32,
+}
+
+/// PcapRecord (src/record.rs:59-65) as a byte offset into the caller's buffer
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_record {
+    pub offset: u64,
+    pub ts_sec: u32,
+    pub ts_usec: u32,
+    pub actual_length: u32,
+    pub original_length: u32,
+}
+
+/// Flow (src/flow/mod.rs:53-61) in the fixed 32-byte encoding
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_flow {
+    pub src_ip: [u8; 4],
+    pub dst_ip: [u8; 4],
+    pub src_port: u16,
+    pub dst_port: u16,
+    pub vlan: u16,
+    pub src_mac: [u8; 6],
+    pub dst_mac: [u8; 6],
+    pub kind: u8,
+    pub record_offset: [u8; 5],
+}
+
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_flow_v6 {
+    pub src_ip: [u8; 16],
+    pub dst_ip: [u8; 16],
+}
+
+extern "C" {
+    pub fn npr_abi_version() -> c_int;
+    pub fn npr_version() -> *const c_char;
+    pub fn npr_ctx_create(device: c_int, out: *mut *mut npr_ctx) -> npr_status;
+    pub fn npr_ctx_destroy(ctx: *mut npr_ctx);
+    pub fn npr_ctx_last_error(ctx: *const npr_ctx) -> *const c_char;
+
+    /// PcapRecords::parse (src/record.rs:21-54)
+    pub fn npr_records_parse(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        endianness: c_int,
+        out: *mut npr_record,
+        cap: usize,
+        n_out: *mut usize,
+        consumed: *mut usize,
+    ) -> npr_status;
+
+    /// FlowExtraction::extract_flow (src/flow/mod.rs:20-48) over a batch of records: dense
+    /// per-record status (npr_flow_status) and flow rows
+    pub fn npr_extract_flows(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        records: *const npr_record,
+        n: usize,
+        flows: *mut npr_flow,
+        flows_v6: *mut npr_flow_v6,
+        status: *mut u8,
+    ) -> npr_status;
+
+    /// flow::convert_records (src/flow/mod.rs:101-123): Ok flows, reverse record order
+    pub fn npr_convert_records(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        records: *const npr_record,
+        n: usize,
+        out: *mut npr_flow,
+        out_v6: *mut npr_flow_v6,
+        cap: usize,
+        n_out: *mut usize,
+    ) -> npr_status;
+
+    /// CaptureFile::parse + convert_records, PCIe transfers pipelined; flows right-aligned in out
+    pub fn npr_parse_extract_pipelined(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        header: *mut npr_global_header,
+        out: *mut npr_flow,
+        out_v6: *mut npr_flow_v6,
+        flow_cap: usize,
+        n_flows: *mut usize,
+        consumed: *mut usize,
+        chunk_bytes: u64,
+    ) -> npr_status;
+
+    pub fn npr_host_alloc(ctx: *mut npr_ctx, bytes: usize, out: *mut *mut c_void) -> npr_status;
+    pub fn npr_host_free(ctx: *mut npr_ctx, p: *mut c_void) -> npr_status;
+}

@@ -1,0 +1,114 @@
+//! `cargo test` on a machine with an MI355X: this crate against the reference crate itself
+//! (net-parser-rs 0.3, a dependency) on the same capture bytes.
+use net_parser_rs_amd as amd;
+
+/// A little-endian capture: Eth/IPv4/TCP and Eth/IPv4/UDP records, one ARP record (never a
+/// flow), one VLAN-tagged record and a truncated tail (the chain stops before it, Q3).
+fn capture() -> Vec<u8> {
+    let mut v = vec![0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0];
+    v.extend_from_slice(&[0u8; 8]);
+    v.extend_from_slice(&65535u32.to_le_bytes());
+    v.extend_from_slice(&1u32.to_le_bytes());
+    for i in 0..5000u32 {
+        let mut f: Vec<u8> = (0..12).map(|k| (i as u8).wrapping_mul(7).wrapping_add(k)).collect();
+        if i % 7 == 3 {
+            f.extend_from_slice(&[0x81, 0x00, 0x00, (i % 4000) as u8]);
+        }
+        if i % 11 == 5 {
+            f.extend_from_slice(&[0x08, 0x06]);
+            f.extend_from_slice(&[1u8; 28]);
+        } else {
+            let udp = i % 2 == 1;
+            f.extend_from_slice(&[0x08, 0x00, 0x45, 0x00]);
+            let l4len: u16 = if udp { 8 + 12 } else { 20 + 10 };
+            f.extend_from_slice(&(20 + l4len).to_be_bytes());
+            f.extend_from_slice(&[0, 0, 0, 0, 64, if udp { 17 } else { 6 }, 0, 0]);
+            f.extend_from_slice(&[10, 0, (i >> 8) as u8, i as u8, 192, 168, 1, (i % 250) as u8]);
+            f.extend_from_slice(&((1000 + i) as u16).to_be_bytes());
+            f.extend_from_slice(&80u16.to_be_bytes());
+            if udp {
+                f.extend_from_slice(&l4len.to_be_bytes());
+                f.extend_from_slice(&[0u8; 2]);
+                f.extend_from_slice(&[9u8; 12]);
+            } else {
+                f.extend_from_slice(&[0u8; 8]);
+                f.extend_from_slice(&[0x50, 0x18]);
+                f.extend_from_slice(&[0u8; 6]);
+                f.extend_from_slice(&[7u8; 10]);
+            }
+        }
+        v.extend_from_slice(&(1_600_000_000 + i / 1000).to_le_bytes());
+        v.extend_from_slice(&(i % 1_000_000).to_le_bytes());
+        v.extend_from_slice(&(f.len() as u32).to_le_bytes());
+        v.extend_from_slice(&(f.len() as u32).to_le_bytes());
+        v.extend_from_slice(&f);
+    }
+    v.extend_from_slice(&[1, 2, 3]); // truncated record header
+    v
+}
+
+fn same_record(a: &net_parser_rs::PcapRecord, b: &net_parser_rs::PcapRecord) -> bool {
+    a.timestamp == b.timestamp
+        && a.actual_length == b.actual_length
+        && a.original_length == b.original_length
+        && a.payload.as_ptr() == b.payload.as_ptr()
+        && a.payload.len() == b.payload.len()
+}
+
+#[test]
+fn capture_file_parse_matches_reference() {
+    let data = capture();
+    let (rem_a, fa) = amd::parse(&data).expect("device parse");
+    let (rem_r, fr) = net_parser_rs::parse(&data).expect("reference parse");
+    assert_eq!(rem_a.len(), rem_r.len());
+    assert_eq!(fa.records.len(), fr.records.len());
+    let (ra, rr) = (fa.records.into_inner(), fr.records.into_inner());
+    assert!(ra.iter().zip(rr.iter()).all(|(a, b)| same_record(a, b)));
+}
+
+#[test]
+fn convert_records_matches_reference() {
+    let data = capture();
+    let (_, fa) = amd::parse(&data).unwrap();
+    let (_, fr) = net_parser_rs::parse(&data).unwrap();
+    let a = amd::flow::convert_records(fa.records.into_inner());
+    let r = net_parser_rs::flow::convert_records(fr.records.into_inner());
+    assert_eq!(a.len(), r.len());
+    for ((ra, fa), (rr, fr)) in a.iter().zip(r.iter()) {
+        assert!(same_record(ra, rr));
+        assert_eq!(fa, fr);
+    }
+    let (_, fa2) = amd::parse(&data).unwrap();
+    let b = amd::flow::convert_records_in(&data, fa2.records.into_inner());
+    assert!(b.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && same_record(&x.0, &y.0)));
+    let (rem, c) = amd::flow::parse_and_convert(&data).unwrap();
+    assert_eq!(rem.len(), 3);
+    assert!(c.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && same_record(&x.0, &y.0)));
+}
+
+#[test]
+fn extract_flow_errors_take_the_reference_variant() {
+    use amd::flow::FlowExtraction as _;
+    let data = capture();
+    let (_, fr) = net_parser_rs::parse(&data).unwrap();
+    for r in fr.records.into_inner().iter().take(40) {
+        let a = amd::flow::FlowExtraction::extract_flow(r);
+        let b = net_parser_rs::flow::FlowExtraction::extract_flow(r);
+        match (a, b) {
+            (Ok(x), Ok(y)) => assert_eq!(x, y),
+            (Err(x), Err(y)) => assert_eq!(format!("{:?}", x).split('{').next(), format!("{:?}", y).split('{').next()),
+            (x, y) => panic!("{:?} vs {:?}", x, y),
+        }
+    }
+}
+
+#[test]
+fn readme_facade() {
+    let data = capture();
+    let recs = amd::CaptureParser::parse_file(&data).expect("Could not parse");
+    assert_eq!(recs.len(), 5000);
+    let packet = amd::CaptureParser::parse_record(&data[24..]).expect("Could not parse");
+    use amd::flow::*;
+    let flow = packet.extract_flow().expect("Could not extract flow");
+    assert_eq!(flow.destination.port, 80);
+}

@@ -42,6 +42,45 @@ def main():
             "flows_out_GBps": round(32 * n_flows / t / 1e9, 2)}
         print(json.dumps({"chunk_KiB": kib, **out["runs"][f"chunk_{kib}KiB" if kib else "one_copy"]}), flush=True)
     ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_STREAM_CHUNK, 0))
+    # npr_parse_extract_pipelined: page-locked chunked H2D | chained launches | per-link D2H,
+    # (a) from a pageable capture (registered per call), (b) from npr_host_alloc'ed buffers
+    cap = n + 1
+    pin_in = device.PinnedArray(len(blob))
+    pin_in.array[:] = a
+    pin_out = device.PinnedArray(cap * 32, _abi.FLOW_DTYPE)
+    page_out = np.zeros(cap, dtype=_abi.FLOW_DTYPE)
+    for label, src, dst in (("pipelined_pageable", a, page_out), ("pipelined_pinned", pin_in.array, pin_out.array)):
+        for mib in (8, 32, 128):
+            device.host_parse_extract_pipelined(src, dst, None, cap, mib << 20, ctx=ctx)
+            ts = []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                flows, _, n_flows, consumed = device.host_parse_extract_pipelined(src, dst, None, cap, mib << 20, ctx=ctx)
+                ts.append(time.perf_counter() - t0)
+            t = min(ts)
+            key = f"{label}_{mib}MiB"
+            out["runs"][key] = {"s": round(t, 5), "Mpackets_per_s": round(n / t / 1e6, 1),
+                                "capture_GBps": round(len(blob) / t / 1e9, 2),
+                                "flows_out_GBps": round(32 * n_flows / t / 1e9, 2)}
+            print(json.dumps({"run": key, **out["runs"][key]}), flush=True)
+    # the raw link: one pinned H2D of the capture, one pinned D2H of the flow table
+    import torch
+    d = torch.empty(len(blob), dtype=torch.uint8, device="cuda")
+    f = torch.empty(cap * 32, dtype=torch.uint8, device="cuda")
+    hin = torch.from_numpy(pin_in.array)
+    hout = torch.from_numpy(pin_out.array.view(np.uint8))
+    for label, fn, nb in (("h2d_pinned", lambda: d.copy_(hin, non_blocking=True), len(blob)),
+                          ("d2h_pinned", lambda: hout.copy_(f, non_blocking=True), cap * 32)):
+        fn(); torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.reps):
+            fn()
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / args.reps
+        out["runs"][label] = {"s": round(t, 5), "GBps": round(nb / t / 1e9, 2)}
+        print(json.dumps({"run": label, **out["runs"][label]}), flush=True)
+    pin_in.close()
+    pin_out.close()
     print(json.dumps(out))
 
 

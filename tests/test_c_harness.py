@@ -1,0 +1,50 @@
+"""The plain-C caller (tests/c_harness/npr_harness.c) of every entry point the Rust crate binds:
+built against include/npr.h + libnpr.so here; run on the GPU (`-m gpu`) over several captures,
+each result checked against the oracle inside the harness."""
+import os
+import subprocess
+
+import pytest
+
+from net_parser_rs import synth
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS_DIR = os.path.join(REPO, "tests", "c_harness")
+HARNESS = os.path.join(HARNESS_DIR, "build", "npr_harness")
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HARNESS_DIR], check=True)
+    return HARNESS
+
+
+def test_harness_builds_and_refuses_without_gpu():
+    import torch
+    exe = build()
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the gpu test runs it")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 2 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_harness_on_device(tmp_path):
+    exe = build()
+    caps = {
+        "c2.pcap": synth.fixed64(50_000),
+        "c3.pcap": synth.variable_mix(5_000),
+        "quirk.pcap": synth.quirk_corpus(5_000, seed=91),
+        "quirk_be.pcap": synth.quirk_corpus(3_000, seed=92, big=True),
+        "adversarial.pcap": synth.quirk_corpus(2_000, seed=93, fake_every=3, zero_every=7, jumbo_every=150,
+                                               tail="truncated_payload"),
+        "short.pcap": synth.global_header()[:20],
+    }
+    paths = []
+    for name, blob in caps.items():
+        p = tmp_path / name
+        p.write_bytes(blob)
+        paths.append(str(p))
+    r = subprocess.run([exe] + paths, capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    print(r.stderr)
+    assert r.returncode == 0 and "OK (0 failures)" in r.stdout
