@@ -210,8 +210,15 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   a chunk ends a link early, which the call detects and answers by parsing the staged capture
  *   again in one go.  Off by default: from pageable host memory the chunked copies measured
  *   slower than one copy, and the copy is ~50x the parse, so overlap gains little.
- * NPR_OPT_PARK_FLOWS: accepted for ABI 2 callers, no effect. */
-enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3 };
+ * NPR_OPT_PARK_FLOWS: accepted for ABI 2 callers, no effect.
+ * NPR_OPT_PIPE (default 0; env NPR_PIPE=1 sets 1 at create): 1 makes the resident flows-only pass the
+ *   pipelined one (tiles dealt round-robin to the persistent waves, each round's convert_records
+ *   rows written while later rounds stream; one launch for any capture size); 0 runs the
+ *   contiguous-range resident pass (one grid-wide prefix, then all rows; chained launches above
+ *   ~100 MB; the default while the pipelined pass measures slower).  Same results
+ *   either way.
+ */
+enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

@@ -38,7 +38,8 @@ struct npr_ctx {
   DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
   int resident = 1;        // NPR_OPT_RESIDENT
   uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
-  uint64_t res_launches = 0;  // resident launches so far (selects the arrival-counter bank)
+  uint32_t pipe_waves = 0; // ... of the pipelined resident pass (a multiple of 15)
+  int pipe = 0;            // NPR_OPT_PIPE: 1 = flows-only launches run k_parse_pipe (0: k_parse_resident)
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
   const npr_summary *sum_ptr[2] = {nullptr, nullptr};  // summaries the last two launches wrote
   uint32_t sum_epoch[2] = {0, 0};
@@ -60,8 +61,8 @@ struct npr_ctx {
 
 namespace {
 
-// control words: abort word [0, 64), two banks of resident-pass arrival counters (65 x 64 B each)
-constexpr size_t kCtlCounters = 64, kCtlBank = 65 * 64, kCtlBytes = kCtlCounters + 2 * kCtlBank;
+// control words: abort word [0, 64), the resident pass's pacing counter [64, 128)
+constexpr size_t kCtlCounters = 64, kCtlBytes = kCtlCounters + 64;
 constexpr uint32_t kTimeoutTicks = 100u * 1000u * 1000u;  // 1 s of s_memrealtime (100 MHz)
 
 npr_status fail(npr_ctx *c, npr_status st, const char *fmt, ...) {
@@ -120,6 +121,8 @@ npr_status res_geometry(npr_ctx *c) {
   HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const int per = npr::resident_waves_per_cu();
   c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
+  const int pper = npr::pipe_waves_per_cu();  // parser waves (15 per workgroup)
+  c->pipe_waves = (uint32_t)std::max<int>((int)npr::kPipeGroupTiles, cus * pper);
   return NPR_OK;
 }
 
@@ -154,7 +157,8 @@ static uint64_t group_slots(uint64_t nt) {
   uint64_t folds = 0;
   for (int l = 1; l <= npr::kLevels; ++l) folds += n[l];
   const uint64_t res = (std::min<uint64_t>(nt, npr::kResMaxWaves) + npr::kResWgMin - 1) / npr::kResWgMin;
-  return std::max(folds, res);
+  const uint64_t pipe = (nt + npr::kPipeGroupTiles - 1) / npr::kPipeGroupTiles;  // k_parse_pipe: one per 15 tiles
+  return std::max(std::max(folds, res), pipe);
 }
 // tile slots, then the group slots: one allocation (granules are epoch-tagged, so the layout may
 // shift between launches)
@@ -181,6 +185,8 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   }
   const char *env = getenv("NPR_RESIDENT");
   if (env && env[0] == '0') c->resident = 0;
+  const char *penv = getenv("NPR_PIPE");
+  if (penv && penv[0]) c->pipe = penv[0] != '0';
   *out = c;
   return NPR_OK;
 }
@@ -218,6 +224,10 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
     case NPR_OPT_RESIDENT:  // 0 off, 1 auto, N > 1: at most N waves (tests: long ranges, deferral)
       if (value < 0) return fail(c, NPR_ERR_ARG, "NPR_OPT_RESIDENT must be >= 0");
       c->resident = value;
+      return NPR_OK;
+    case NPR_OPT_PIPE:  // 1: flows-only launches run the pipelined resident pass (default 0)
+      if (value < 0 || value > 1) return fail(c, NPR_ERR_ARG, "NPR_OPT_PIPE must be 0 or 1");
+      c->pipe = value;
       return NPR_OK;
     case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first
       if (value < 0 || (value > 0 && value < 64)) return fail(c, NPR_ERR_ARG, "NPR_OPT_STREAM_CHUNK: 0 or >= 64 KiB");
@@ -304,7 +314,7 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness e, const npr_dev_outputs *o, void *stream) {
   // flows-only captures larger than one launch keeps in registers: chained chunks of that size
-  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start) {
+  if (c && o && c->resident && !c->pipe && !o->record_offsets && !o->records && !o->record_status && len > start) {
     npr_status st = res_geometry(c);
     if (st) return st;
     if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
@@ -487,7 +497,21 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
       }
     }
   }
-  if (resident) {
+  if (resident && c->pipe) {  // the pipelined pass: whole workgroups of 15 parsers, tiles dealt round-robin
+    if ((st = res_geometry(c))) return st;
+    const uint64_t G = npr::kPipeGroupTiles;
+    uint64_t wv = std::min<uint64_t>(nt, c->pipe_waves);
+    if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
+    wv = std::min<uint64_t>((wv + G - 1) / G * G, c->pipe_waves / G * G);
+    p.nwaves = (uint32_t)wv;
+    p.pipe = 1;
+    p.rslots = (npr::RangeSlot *)c->slots.p;  // one per tile
+    p.rgroups = p.groups[1];                  // G(q, b) at q * workgroups + b: one per 15 tiles
+    const uint64_t ng = (nt + npr::kPipeGroupTiles - 1) / npr::kPipeGroupTiles;
+    if ((const char *)(p.rgroups + ng) > (const char *)c->slots.p + c->slots.cap)
+      return fail(c, NPR_ERR_ARG, "internal: pipelined group slots exceed the workspace (%llu groups)",
+                  (unsigned long long)ng);
+  } else if (resident) {
     if ((st = res_geometry(c))) return st;
     uint64_t wv = std::min<uint64_t>(nt, c->res_waves);
     if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
@@ -499,9 +523,7 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     if ((const char *)(p.rgroups + nb) > (const char *)c->slots.p + c->slots.cap)
       return fail(c, NPR_ERR_ARG, "internal: resident workgroup slots exceed the workspace (%llu groups)",
                   (unsigned long long)nb);
-    const uint64_t bank = c->res_launches++ & 1u;  // this launch counts in a bank the previous one zeroed
-    p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters + bank * kCtlBank);
-    p.rcnt_next = (uint32_t *)((char *)c->abort_word + kCtlCounters + (bank ^ 1u) * kCtlBank);
+    p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
   }
   HIP_CHECK(c, npr::launch_parse_extract(p, s));
   c->sum_ptr[c->sum_next] = o->summary;  // who wrote which summary (chained launches check it)

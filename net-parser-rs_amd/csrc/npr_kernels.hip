@@ -12,19 +12,22 @@
 //     per-layer flow dispatch         src/flow/layer2/ethernet.rs:39-133, src/flow/layer3/*.rs
 //   flow::convert_records             src/flow/mod.rs:101-123 -> reverse-order rows, ranked by ballot
 //
-// Design: two streaming passes of ONE-WAVE workgroups, one per 4 KiB tile, each
-// tile staged into LDS by DMA (no workgroup barriers, no waits on other tiles in the common case).
-//   pass 1 (k_count_tiles): a tile's entry is SPECULATED from header plausibility (tile 0 starts
-//     at `start`); the wave walks the chain (stride speculation, up to 256 records per step),
-//     decodes every record's status and publishes A = {entry, exit, records, Ok flows}.  The
-//     wave that finishes a group's last tile folds the group (64 tiles, then 64 groups, then 64
-//     blocks) with a chain-consistency monoid: the group's aggregate and every member's
-//     exclusive prefix inside it;
-//   pass 2 (k_emit_tiles): the exact chain state before a tile is the anchor folded with its
-//     three exclusive prefixes (point loads issued beside the tile's DMA); a contradiction waits
-//     for the offending tile's exact prefix P, which its own wave publishes in this pass; every
-//     record is decoded from the exact position (reusing pass 1's offsets when its entry was
-//     right) and its Ok flow goes straight to its reverse-order (convert_records) row.
+// Design.  A 4 KiB TILE of the record stream is the unit of work; every tile is
+// staged into LDS by DMA and its entry (first record start) is SPECULATED from header plausibility
+// (tile 0 starts at `start`); a wave walks the chain from it, decodes every record's flow status
+// and summarises the tile as A = {entry, exit, records, Ok flows}.  Tiles combine under a
+// chain-consistency monoid (an aggregate is exact when each entry continues its predecessor's
+// exit).  Three launch shapes use these pieces:
+//   k_count_tiles + k_emit_tiles (record-table launches): two streaming passes of one-wave
+//     workgroups, one per tile; pass 1 publishes A and folds 64-tile groups, pass 2 rebuilds the
+//     exact state before each tile from the folds and writes every record row and flow;
+//   k_parse_resident (flows-only launches, NPR_PIPE=0): persistent waves, each owning a
+//     contiguous tile range, flows kept in registers; one pass with a decoupled look-back over
+//     16-wave workgroup aggregates;
+//   k_parse_pipe (flows-only launches, default): persistent workgroups of 15 parser waves + 1
+//     resolver wave; tiles are dealt round-robin (tile = round * parsers + parser), so every
+//     round is a contiguous slab of the capture; the resolver folds each round's aggregates and
+//     posts every parser's exact prefix while the parsers stream on (npr_kernels_pipe.inc).
 // A wrong speculation costs a wait or a re-walk, never a wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -372,7 +375,7 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 struct Seg {
   uint64_t entry, exit, cnt, ok;
   int64_t first, last, mism;  // mism: lowest tile whose speculated entry is contradicted
-  bool valid;
+  uint32_t valid, spare;      // (no padding bytes: a padded copy is left in scratch memory)
 };
 
 __device__ __forceinline__ uint64_t tile_end(const ParseParams &kp, int64_t k) {
@@ -426,7 +429,7 @@ __device__ __forceinline__ uint64_t *prefix_words(const ParseParams &kp, int lvl
 struct LaneSeg {
   uint64_t entry, exit, cnt, ok;
   int64_t first, last, mism;
-  bool valid, present;
+  uint32_t valid, present;  // (32-bit: no padding bytes)
 };
 
 // level 0: A = {exit, entry + 1, n | okc << 24};  levels 1..3: G = {exit, entry + 1, cnt, ok | valid << 32, mism + 1}
@@ -1320,7 +1323,7 @@ constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
 #define NPR_RES_WG 16
 #endif
 constexpr uint32_t kResWg = NPR_RES_WG;   // waves per workgroup (one workgroup per CU): folded in LDS
-static_assert(kResWg >= kResWgMin, "ready granules are sized for kResWgMin");
+static_assert(kResWg >= kResWgMin, "workgroup aggregate slots (npr_capi.hip group_slots) are sized for kResWgMin");
 static_assert(kResRing >= 2 && (kResRing - 1) * kDmaPer < 64, "vmcnt field is 6 bits");
 
 struct ResShared {  // one wave's LDS
@@ -1437,9 +1440,8 @@ __device__ bool res_fold(const ParseParams &kp, int lvl, int64_t base, int cnt, 
   }
 }
 
-// Arrival counter: returns the count including this arrival.  Each launch counts in a bank the
-// previous resident launch zeroed (the host alternates two banks).  Callers ran
-// `s_waitcnt vmcnt(0)` after the stores the arrival vouches for.
+// Pacing arrival on the launch's one counter word: a returning atomic whose round trip delays
+// the caller's first look-back read.  Nothing reads the count (it wraps freely).
 __device__ __forceinline__ uint32_t res_arrive(uint32_t *ctr) {
   return __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
 }
@@ -1675,10 +1677,6 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   if (active) res_range(kp, v, c0, c1);
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
   const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;  // chained: tile 0 speculates too
-  if (v == 0) {  // zero the other counter bank for the next resident launch
-    kp.rcnt_next[16u * lane] = 0u;
-    if (lane == 0) kp.rcnt_next[16u * 64u] = 0u;
-  }
   if (threadIdx.x == 0) sh.fail = 0;
   const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
 #pragma unroll
@@ -1831,7 +1829,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     // arrival's round trip only paces the first window read below (measured 0.3 us better than
     // reading at once, which re-reads more aggregates that are not published yet)
     if (lane == 0) put_agg(kp, kp.rgroups + b, agg);
-    if (lane == 0) (void)res_arrive(kp.rcnt + 16u * 64u);
+    if (lane == 0) (void)res_arrive(kp.rcnt);
     if (DIAG) stamp_at(st, 3);
     // (2) E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1), looking back: every window read at once, then
     //     only the aggregates that are not this launch's yet re-read, until all are (a workgroup
@@ -1969,6 +1967,16 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   }
 }
 
+#include "npr_kernels_pipe.inc"
+
+int pipe_waves_per_cu() {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_pipe<false>), kPipeWg * kWave, 0) !=
+      hipSuccess)
+    return 0;
+  return nb * (int)kPipePar;  // parser waves
+}
+
 int resident_waves_per_cu() {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false>), kResWg * kWave, 0) !=
@@ -1987,6 +1995,12 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
 }
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
+  if (p.nwaves && p.pipe) {
+    const uint32_t nb = p.nwaves / kPipePar;
+    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_pipe<true>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
+    else hipLaunchKernelGGL((k_parse_pipe<false>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
+    return hipGetLastError();
+  }
   if (p.nwaves) {
     const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
     if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_resident<true>), dim3(nb), dim3(kResWg * kWave), 0, s, p);

@@ -35,6 +35,7 @@ KIND_UDP = 0x2
 OK, INCOMPLETE, FAILURE, CUSTOM = 0, 1, 2, 3
 OPT_PARK_FLOWS = 1  # npr_ctx_set_option: accepted for ABI 2 callers, no effect
 OPT_RESIDENT = 2    # npr_ctx_set_option: flows-only parses run the resident single pass (0 off, 1 auto, N>1 cap)
+OPT_PIPE = 4  # npr_ctx_set_option: flows-only parses run the pipelined resident pass (1) or the contiguous one (0, default)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1

@@ -4,7 +4,8 @@ Every case runs the fused device kernel (npr_dev_parse_extract) and compares: th
 (offset, ts, lengths), per-record flow status, the convert_records flow table (bytes, incl. IPv6
 side table), n_records / n_flows and `consumed` (the Rust remainder).  Inputs are seeded
 synthetic captures (net_parser_rs.synth) sized so the oracle finishes in seconds, plus the
-reference's own KAT frames.  Full-size configs are checked through properties (test_gpu_full.py).
+reference's own KAT frames.  Full-size configs (C2 1M, C3 8M, C4 16M/64M, the C5 tiled corpus) are
+checked bit-exact or per shard in test_gpu_scale.py.
 """
 import json
 import os
@@ -39,7 +40,19 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     default for flows-only launches); light=N (an int > 1) the same with at most N waves, so
     each wave owns a long tile range (kept-round overflow -> deferred tiles, many ranges per
     64-wave group, speculation at range starts deep inside the capture); light="decode" the
-    two-pass kernels (NPR_OPT_RESIDENT off)."""
+    two-pass kernels (NPR_OPT_RESIDENT off); light="pipe" / "pipe_wN" the pipelined resident pass
+    (k_parse_pipe, NPR_OPT_PIPE on), the latter with at most N parser waves (many rounds per
+    parser: kept-slot flushes, deferred rounds, the resolver's generic path)."""
+    if isinstance(light, str) and light.startswith("pipe"):
+        ctx = npr.context(0)
+        cap = int(light[6:]) if light.startswith("pipe_w") else 1
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 1))
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, cap))
+        try:
+            return check_parity(blob, start, endianness, ws, light=True)
+        finally:
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 0))
     if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
         ctx = npr.context(0)
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
@@ -118,8 +131,9 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, "decode"],
-                                ids=["full", "resident", "resident_w7", "resident_w100", "two_pass"])
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, "decode", "pipe", "pipe_w30", "pipe_w150"],
+                                ids=["full", "resident", "resident_w7", "resident_w100", "two_pass", "pipe",
+                                     "pipe_w30", "pipe_w150"])
 
 
 @LIGHT
@@ -333,8 +347,9 @@ def test_capture_past_2GiB():
     del blob
     ctx = npr.context(0)
     try:
-        for resident in (1, 0):
+        for resident, pipe in ((1, 0), (1, 1), (0, 0)):
             ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, resident))
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, pipe))
             w = device.Workspace(n + 1, n + 1, records=False, status=False)
             w.launch(buf, start=24, endianness=hdr.endianness)
             sm = w.check()
@@ -344,3 +359,4 @@ def test_capture_past_2GiB():
             del w
     finally:
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 0))
