@@ -351,6 +351,13 @@ npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
 npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
                                  const npr_record *records, uint64_t n, npr_flow *flows,
                                  npr_flow_v6 *flows_v6, uint8_t *status, void *stream);
+/* flow::convert_records (src/flow/mod.rs:101-123) over device-resident records, asynchronous on
+ * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
+ * cap are not written), *n_out (a device word) = the number of Ok flows, or UINT64_MAX when the
+ * launch's bounded look-back timed out.  One kernel pass. */
+npr_status npr_dev_convert_records(npr_ctx *ctx, const void *input, uint64_t len,
+                                   const npr_record *records, uint64_t n, npr_flow *out,
+                                   npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream);
 
 #ifdef __cplusplus
 }

@@ -45,7 +45,7 @@ struct npr_ctx {
   uint32_t sum_epoch[2] = {0, 0};
   uint32_t sum_next = 0;
   // staging for the host-memory entry points
-  DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, scratch;
+  DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6;
   // host flows-only parses: the capture's H2D copy in chunks on copy_stream, each chunk's chained
   // launch as soon as its bytes (and the next chunk's, for records that straddle) have landed
   uint64_t stream_chunk = 0;  // NPR_OPT_STREAM_CHUNK (KiB in the option; 0 = one copy, the default)
@@ -102,6 +102,17 @@ npr_status ensure(npr_ctx *c, DevBuf &b, size_t bytes, bool zero = false) {
   b.cap = want;
   return NPR_OK;
 }
+
+// The next granule tag (1..65535) for a launch on stream s; on wrap every slot is cleared once.
+static npr_status next_epoch(npr_ctx *c, hipStream_t s) {
+  if (++c->epoch > 0xffffu) {
+    c->epoch = 1;
+    HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
+    HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, kCtlBytes, s));
+  }
+  return NPR_OK;
+}
+
 
 inline uint32_t rd_u32(const uint8_t *p, bool big) {
   uint32_t v;
@@ -196,7 +207,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->chain, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
-                    &c->flows2_v6, &c->scratch})
+                    &c->flows2_v6})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
   if (c->summary) (void)hipFree(c->summary);
@@ -424,11 +435,7 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
   if (st) return st;
   if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
   hipStream_t s = pick(c, stream);
-  if (++c->epoch > 0xffffu) {  // granule tags wrap: clear every slot once per 65535 launches
-    c->epoch = 1;
-    HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
-    HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, kCtlBytes, s));
-  }
+  if ((st = next_epoch(c, s))) return st;
   npr::ParseParams p{};
   p.buf = (const uint8_t *)input - base;  // buf + o = file byte o (only o >= base is ever read)
   p.base = base;
@@ -543,6 +550,25 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   }
   if (c->summary_h->flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded (flags=%u)", c->summary_h->flags);
   return NPR_OK;
+}
+
+// convert_records over device records: one pass, look-back words in the slot allocation
+static npr_status convert_launch(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
+                                 npr_flow *out, npr_flow_v6 *out_v6, uint64_t cap, uint64_t *total, hipStream_t s) {
+  npr_status st = ensure(c, c->slots, std::max<uint64_t>(npr::convert_look_words(n), 1) * 8, true);
+  if (st) return st;
+  if ((st = next_epoch(c, s))) return st;
+  HIP_CHECK(c, npr::launch_convert_records((const uint8_t *)input, len, recs, n, (uint32_t *)out, (uint32_t *)out_v6,
+                                           cap, (uint64_t *)c->slots.p, c->epoch, total,
+                                           kTimeoutTicks, s));
+  return NPR_OK;
+}
+
+npr_status npr_dev_convert_records(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
+                                   npr_flow *out, npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream) {
+  if (!c || (!input && len) || (!recs && n) || !n_out || (!out && cap)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  return convert_launch(c, input, len, recs, n, out, out_v6, cap, n_out, pick(c, stream));
 }
 
 npr_status npr_dev_extract_flows(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs,
@@ -907,24 +933,17 @@ npr_status npr_convert_records(npr_ctx *c, const uint8_t *in, size_t len, const 
   }
   const uint64_t ocap = std::min<uint64_t>(cap, n);
   if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
-  if ((st = ensure(c, c->flows, n * sizeof(npr_flow)))) return st;
-  if ((st = ensure(c, c->flows_v6, n * sizeof(npr_flow_v6)))) return st;
-  if ((st = ensure(c, c->status, n))) return st;
   if ((st = ensure(c, c->flows2, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow)))) return st;
   if ((st = ensure(c, c->flows2_v6, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow_v6)))) return st;
-  if ((st = ensure(c, c->scratch, npr::compact_workspace_words(n) * 4 + 64))) return st;
   HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
-  HIP_CHECK(c, npr::launch_extract_dense((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n,
-                                         (uint32_t *)c->flows.p, (uint32_t *)c->flows_v6.p, (uint8_t *)c->status.p,
-                                         c->stream));
   uint64_t *total = (uint64_t *)c->summary;  // scratch word
-  HIP_CHECK(c, npr::launch_compact_reverse((const uint32_t *)c->flows.p, (const uint32_t *)c->flows_v6.p,
-                                           (const uint8_t *)c->status.p, n, (uint32_t *)c->flows2.p,
-                                           (uint32_t *)c->flows2_v6.p, ocap, (uint32_t *)c->scratch.p, total,
-                                           c->stream));
+  if ((st = convert_launch(c, c->in.p, len, (const npr_record *)c->recs.p, n, (npr_flow *)c->flows2.p,
+                           out_v6 ? (npr_flow_v6 *)c->flows2_v6.p : nullptr, ocap, total, c->stream)))
+    return st;
   uint64_t tot = 0;
   HIP_CHECK(c, hipMemcpyAsync(&tot, total, 8, hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  if (tot == ~0ull) return fail(c, NPR_ERR_TIMEOUT, "convert_records did not complete (look-back timed out)");
   const uint64_t k = std::min<uint64_t>(tot, ocap);
   if (k) {
     if (out) HIP_CHECK(c, hipMemcpyAsync(out, c->flows2.p, k * sizeof(npr_flow), hipMemcpyDeviceToHost, c->stream));

@@ -135,11 +135,12 @@ constexpr uint32_t kPipeGroupTiles = 15;  // tiles per group slot of the pipelin
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);
-// convert_records over a dense extract: Ok rows of (flows, flows_v6, status) in reverse order.
-hipError_t launch_compact_reverse(const uint32_t *flows, const uint32_t *flows_v6,
-                                  const uint8_t *status, uint64_t n, uint32_t *out,
-                                  uint32_t *out_v6, uint64_t cap, uint32_t *block_counts,
-                                  uint64_t *total, hipStream_t s);
-uint64_t compact_workspace_words(uint64_t n);
+// convert_records in one pass (k_convert_records): rows 0.. = Ok flows in reverse record order,
+// *total = all Ok flows (rows past cap are not written; ~0 when a bounded wait timed out).
+// look: convert_look_words(n) granules whose tags are not `epoch` at launch.
+hipError_t launch_convert_records(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
+                                  uint32_t *out, uint32_t *out_v6, uint64_t cap, uint64_t *look, uint32_t epoch,
+                                  uint64_t *total, uint64_t timeout_ticks, hipStream_t s);
+uint64_t convert_look_words(uint64_t n);
 
 }  // namespace npr

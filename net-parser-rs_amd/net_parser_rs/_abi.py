@@ -98,6 +98,7 @@ EXPORTED = [
     "npr_parse_extract_pipelined", "npr_host_alloc", "npr_host_free",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
+    "npr_dev_convert_records",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -146,6 +147,8 @@ _SIGNATURES = {
     "npr_dev_check": (ctypes.c_int, [_vp, ctypes.POINTER(DevOutputsC), _vp, ctypes.POINTER(SummaryC)]),
     "npr_dev_extract_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                              _vp, _vp, _vp, _vp]),
+    "npr_dev_convert_records": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
+                                               _vp, _vp, ctypes.c_uint64, _vp, _vp]),
 }
 
 _lib = None

@@ -152,6 +152,51 @@ def parse_extract(buf, start=24, endianness=_abi.LITTLE, record_cap=None, flow_c
     return Result(ws, sm)
 
 
+def _dev_records(recs):
+    """A device npr_record table: a CUDA uint8 tensor of n * 24 bytes (or int64 of n * 3)."""
+    assert recs.is_cuda and recs.is_contiguous()
+    nbytes = recs.numel() * recs.element_size()
+    assert nbytes % 24 == 0 and recs.data_ptr() % 8 == 0
+    return nbytes // 24
+
+
+def dev_extract_flows(buf, recs, flows=None, flows_v6=None, status=None, ctx=None, stream=None):
+    """FlowExtraction::extract_flow per record over device-resident records (npr_dev_extract_flows),
+    async on `stream`: dense (flows, flows_v6, status) tensors, row i for record i (zero rows where
+    the status is not Ok)."""
+    n = _dev_records(recs)
+    dev = buf.device
+    mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    flows = mk(n * 32) if flows is None else flows
+    flows_v6 = mk(n * 32) if flows_v6 is None else flows_v6
+    status = mk(n) if status is None else status
+    ctx = ctx if ctx is not None else context(dev.index or 0)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    ctx.check(ctx.lib.npr_dev_extract_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
+                                            flows.data_ptr(), flows_v6.data_ptr(), status.data_ptr(),
+                                            ctypes.c_void_p(s.cuda_stream)))
+    return flows, flows_v6, status
+
+
+def dev_convert_records(buf, recs, cap=None, out=None, out_v6=None, with_v6=True, ctx=None, stream=None):
+    """flow::convert_records over device-resident records (npr_dev_convert_records), async on
+    `stream`: (out, out_v6 or None, n_out) where rows [0, min(n_out, cap)) are the Ok flows in
+    reverse record order and n_out is a one-element CUDA int64 tensor (-1 = UINT64_MAX: timed out)."""
+    n = _dev_records(recs)
+    dev = buf.device
+    cap = n if cap is None else int(cap)
+    mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    out = mk(cap * 32) if out is None else out
+    out_v6 = (mk(cap * 32) if out_v6 is None else out_v6) if with_v6 else None
+    n_out = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx = ctx if ctx is not None else context(dev.index or 0)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    ctx.check(ctx.lib.npr_dev_convert_records(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
+                                              out.data_ptr(), out_v6.data_ptr() if out_v6 is not None else None,
+                                              cap, n_out.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    return out, out_v6, n_out
+
+
 def host_parse_extract(data, flow_cap=None, with_v6=True, ctx=None):
     """npr_parse_extract without a record table: a host capture (bytes / uint8 array) in, the
     convert_records flow table out on the host.  Captures of more than two NPR_OPT_STREAM_CHUNK

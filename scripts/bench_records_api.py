@@ -1,0 +1,112 @@
+"""Per-record entry points on the C2 capture (1M x 64-B records): device time of
+npr_dev_convert_records and npr_dev_extract_flows (HIP events around K launches on one stream),
+the host-memory npr_convert_records call (PCIe included), and the CPU oracle's convert_records
+over the same record list.  Prints one JSON line.
+
+Algorithmic bytes per record: 24 (the npr_record row) + 64 (the frame the decode reads) read,
+32 (flow row) + 32 (IPv6 side row) written for convert (Ok rows only), dense extract also 1 B of
+status.  Usage: python scripts/bench_records_api.py [--records N] [--steps K]"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "net-parser-rs_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import _oracle  # noqa: E402
+import net_parser_rs as npr  # noqa: E402
+from net_parser_rs import _abi, device, synth  # noqa: E402
+
+
+def timed_events(fn, steps, stream):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=50)
+    args = ap.parse_args()
+    n = args.records
+    blob = synth.fixed64(n)
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    assert rc == 0 and len(recs) == n
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    buf = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).to(dev)
+    drecs = torch.from_numpy(recs.view(np.uint8).copy()).to(dev)
+    out = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    out6 = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    f = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    f6 = torch.empty(n * 32, dtype=torch.uint8, device=dev)
+    st = torch.empty(n, dtype=torch.uint8, device=dev)
+    ctx = npr.context(0)
+
+    # correctness gate: the measured launch against the oracle
+    want_f, want_v6 = _oracle.convert_records(blob, recs)
+    _, _, n_out = device.dev_convert_records(buf, drecs, cap=n, out=out, out_v6=out6, ctx=ctx, stream=stream)
+    torch.cuda.synchronize()
+    assert int(n_out.item()) == len(want_f) and out.cpu().numpy().tobytes() == want_f.tobytes()
+
+    cvt_ms = timed_events(lambda: device.dev_convert_records(buf, drecs, cap=n, out=out, out_v6=out6, ctx=ctx,
+                                                             stream=stream), args.steps, stream)
+    ext_ms = timed_events(lambda: device.dev_extract_flows(buf, drecs, f, f6, st, ctx=ctx, stream=stream),
+                          args.steps, stream)
+    # host-memory call (pageable buffers; PCIe in and out)
+    a = np.frombuffer(blob, np.uint8)
+    hf = np.zeros(n, _abi.FLOW_DTYPE)
+    h6 = np.zeros(n, _abi.FLOW_V6_DTYPE)
+    k = ctypes.c_size_t(0)
+    call = lambda: ctx.check(ctx.lib.npr_convert_records(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n,
+                                                         hf.ctypes.data, h6.ctypes.data, n, ctypes.byref(k)))
+    call()
+    reps = 5
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    host_ms = (time.perf_counter() - t0) * 1e3 / reps
+    assert k.value == len(want_f) and hf.tobytes() == want_f.tobytes()
+    # the CPU oracle on the same list
+    t0 = time.perf_counter()
+    passes = 0
+    while time.perf_counter() - t0 < 5.0:
+        _oracle.convert_records(blob, recs)
+        passes += 1
+    cpu_ms = (time.perf_counter() - t0) * 1e3 / passes
+
+    cvt_bytes = n * (24 + 64) + len(want_f) * 64
+    ext_bytes = n * (24 + 64 + 64 + 1)
+    res = {
+        "workload": f"C2 record list ({n} x 64-B frames), records + capture resident in HBM",
+        "dev_convert_records": {"kernel_ms": round(cvt_ms, 5), "Mrecords_per_s": round(n / cvt_ms / 1e3, 1),
+                                "alg_bytes": cvt_bytes, "GBps": round(cvt_bytes / cvt_ms / 1e6, 1),
+                                "frac_of_8TBps": round(cvt_bytes / cvt_ms / 1e6 / 8000, 4)},
+        "dev_extract_flows": {"kernel_ms": round(ext_ms, 5), "Mrecords_per_s": round(n / ext_ms / 1e3, 1),
+                              "alg_bytes": ext_bytes, "GBps": round(ext_bytes / ext_ms / 1e6, 1),
+                              "frac_of_8TBps": round(ext_bytes / ext_ms / 1e6 / 8000, 4)},
+        "host_convert_records": {"ms": round(host_ms, 3), "Mrecords_per_s": round(n / host_ms / 1e3, 1),
+                                 "note": "pageable host buffers: capture + records H2D, flow rows D2H"},
+        "cpu_oracle_convert_records": {"ms": round(cpu_ms, 3), "Mrecords_per_s": round(n / cpu_ms / 1e3, 2),
+                                       "cores": 1, "passes": passes},
+    }
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -9,9 +9,12 @@ if [ -n "$K" ]; then
 else
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || exit $?
 fi
-timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu > gpurun_out/bench_c2_$TAG.json 2> gpurun_out/bench_c2_$TAG.err || exit $?
+NPR_PIPE=1 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu > gpurun_out/bench_c2_$TAG.json 2> gpurun_out/bench_c2_$TAG.err || exit $?
 NPR_PIPE=0 timeout -k 10 300 python bench.py --steps 50 --warmup 10 --no-cpu > gpurun_out/bench_c2_$TAG.old.json 2>> gpurun_out/bench_c2_$TAG.err || exit $?
-timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --stats > gpurun_out/bench_c2_$TAG.stats.json 2>> gpurun_out/bench_c2_$TAG.err || exit $?
+NPR_PIPE=1 timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu --stats > gpurun_out/bench_c2_$TAG.stats.json 2>> gpurun_out/bench_c2_$TAG.err || exit $?
 python scripts/pipe_stamps.py > gpurun_out/pipe_stamps_$TAG.txt 2>&1 || exit $?
-timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 2 --no-cpu > gpurun_out/bench_c3_$TAG.json 2> gpurun_out/bench_c3_$TAG.err || exit $?
+NPR_PIPE=1 timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 2 --no-cpu > gpurun_out/bench_c3_$TAG.json 2> gpurun_out/bench_c3_$TAG.err || exit $?
+for per in 4; do
+  NPR_CVT_PER=$per timeout -k 10 300 python scripts/bench_records_api.py > gpurun_out/records_api_$TAG.per$per.json 2>> gpurun_out/records_api_$TAG.err || exit $?
+done
 exit 0

@@ -1,7 +1,8 @@
 """Timeline of one k_parse_pipe launch from its DIAG stamps (bench.py --stats -> gpurun_out/stamps_rank0.npy).
 Parser row v: [0] start [1..6] round 0..5 aggregate published [7] drain start [8] done [9] ticks in blocking
 flushes [10] rounds flushed before the drain [11] rounds.  Resolver row W + b: [q] round q's X posted
-(q < 12), [12] round 0 arrivals complete, [13] round 0 G(0, b) published, [14] round 0 G windows folded.
+(q < 8), [12] / [13] G(0, b) / G(1, b) published, [14] / [8] every G(0, .) / G(1, .) seen, [10] / [9]
+round 0 / 1 windows folded, [11] round 0 local fold done.
 Usage: python scripts/pipe_stamps.py [path] [W]"""
 import sys
 
@@ -32,8 +33,12 @@ row("parser drain start", 7)
 row("parser done", 8)
 row("parser blocking-flush us", 9, rel=False)
 print("rounds flushed before drain (median):", np.median(par[:, 10]), " rounds:", np.bincount(par[:, 11]))
-row("resolver round0 arrivals", 12, res)
-row("resolver round0 G published", 13, res)
-row("resolver round0 folded", 14, res)
+row("resolver G(0,b) published", 12, res)
+row("resolver G(0,.) all seen", 14, res)
+row("resolver round0 windows folded", 10, res)
+row("resolver round0 local fold", 11, res)
+row("resolver G(1,b) published", 13, res)
+row("resolver G(1,.) all seen", 8, res)
+row("resolver round1 windows folded", 9, res)
 for q in range(8):
     row(f"resolver round {q} X posted", q, res)

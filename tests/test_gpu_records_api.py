@@ -1,0 +1,121 @@
+"""Per-record entry points over device-resident records, bit-exact against the oracle.
+
+npr_dev_extract_flows (FlowExtraction::extract_flow per record, src/flow/mod.rs:20-48) and
+npr_dev_convert_records (flow::convert_records, src/flow/mod.rs:101-123: Ok flows in REVERSE
+record order) take an arbitrary npr_record list, so the cases go past what a parse produces:
+permuted lists, payloads shortened to a prefix of the frame, records that do not lie inside the
+buffer, payloads ending at the buffer's last byte (the staged 96-B window falls back to global
+bytes), output capacity below the Ok count, and list lengths around the 256-record block.
+"""
+import numpy as np
+import pytest
+import torch
+
+from net_parser_rs import _abi, device, synth
+
+import _oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).copy()).cuda()
+
+
+def records_of(blob, shrink=0.0, permute=False, seed=0):
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    assert rc == 0
+    recs = recs.copy()
+    rng = np.random.default_rng(seed)
+    if shrink:
+        m = rng.random(len(recs)) < shrink
+        recs["actual_length"][m] = (recs["actual_length"][m] * rng.random(m.sum())).astype(np.uint32)
+    if permute:
+        recs = recs[rng.permutation(len(recs))]
+    return recs
+
+
+def check_dense(blob, recs):
+    want_f, want_v6, want_st = _oracle.extract_flows(blob, recs)
+    n = len(recs)
+    f, f6, st = device.dev_extract_flows(dev(np.frombuffer(blob, np.uint8)), dev(recs))
+    torch.cuda.synchronize()
+    assert np.array_equal(st[:n].cpu().numpy(), want_st)
+    assert f[: n * 32].cpu().numpy().tobytes() == want_f.tobytes()
+    assert f6[: n * 32].cpu().numpy().tobytes() == want_v6.tobytes()
+
+
+def check_convert(blob, recs, cap=None, with_v6=True):
+    want_f, want_v6 = _oracle.convert_records(blob, recs)
+    k = len(want_f)
+    n = len(recs)
+    cap = n if cap is None else cap
+    out, out6, n_out = device.dev_convert_records(dev(np.frombuffer(blob, np.uint8)), dev(recs), cap=cap,
+                                                  with_v6=with_v6)
+    torch.cuda.synchronize()
+    assert int(n_out.item()) == k
+    w = min(k, cap)
+    assert out[: w * 32].cpu().numpy().tobytes() == want_f[:w].tobytes()
+    if with_v6:
+        assert out6[: w * 32].cpu().numpy().tobytes() == want_v6[:w].tobytes()
+    return k
+
+
+CORPORA = {
+    "quirk": lambda: synth.quirk_corpus(8_000, seed=3),
+    "quirk_be": lambda: synth.quirk_corpus(5_000, seed=11, big=True),
+    "c2": lambda: synth.fixed64(50_000),
+    "c3": lambda: synth.variable_mix(20_000),
+    "adversarial": lambda: synth.quirk_corpus(4_000, seed=5, fake_every=3, zero_every=7, jumbo_every=200),
+}
+
+
+@pytest.mark.parametrize("name", sorted(CORPORA))
+@pytest.mark.parametrize("variant", ["parsed", "shrunk_permuted"])
+def test_dev_per_record_matches_oracle(name, variant):
+    blob = CORPORA[name]()
+    recs = records_of(blob, shrink=0.2, permute=True, seed=7) if variant != "parsed" else records_of(blob)
+    check_dense(blob, recs)
+    assert check_convert(blob, recs) > 0 or name == "adversarial"
+
+
+@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 511, 513, 64 * 256 + 3])
+def test_dev_convert_block_edges(n):
+    blob = synth.fixed64(max(n, 1))
+    recs = records_of(blob)[:n]
+    if n:
+        check_dense(blob, recs)
+    assert check_convert(blob, recs) == n  # every fixed64 frame is an Ok flow
+
+
+def test_dev_convert_capacity_below_count():
+    blob = synth.variable_mix(30_000)
+    recs = records_of(blob)
+    k = check_convert(blob, recs, cap=1000)
+    assert k > 1000
+    check_convert(blob, recs, cap=0)
+    check_convert(blob, recs, with_v6=False)
+
+
+def test_records_outside_the_buffer_and_at_its_end():
+    """Records past the buffer (status 0xff, never a flow), and the buffer cut right after a
+    frame so the last payloads end at its final byte (window past the end -> global bytes)."""
+    blob = synth.quirk_corpus(3_000, seed=21)
+    recs = records_of(blob)
+    last = recs[-1]
+    cut = blob[: int(last["offset"]) + 16 + int(last["actual_length"])]
+    check_dense(cut, recs)
+    check_convert(cut, recs)
+    bad = recs[:300].copy()
+    bad["offset"][::3] += len(blob)                       # header past the end
+    bad["actual_length"][1::3] = len(blob)                # payload past the end
+    check_dense(blob, bad)
+    check_convert(blob, bad)
+
+
+def test_dev_convert_c2_full_size():
+    """The C2 bench capture (1M 64-B frames): every record, one launch, bit-exact."""
+    blob = synth.fixed64(1_000_000)
+    recs = records_of(blob)
+    assert check_convert(blob, recs) == 1_000_000
+    check_dense(blob, recs)
