@@ -55,6 +55,7 @@ struct npr_ctx {
   hipStream_t d2h_stream = nullptr;
   std::vector<hipEvent_t> linked;
   npr_summary *sum_host = nullptr;
+  uint8_t *head_h = nullptr;  // pinned: the first bytes of a large capture (link sizing)
   uint64_t sum_host_cap = 0;
   std::string err;
 };
@@ -218,6 +219,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   for (hipEvent_t ev : c->copied) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : c->linked) (void)hipEventDestroy(ev);
   if (c->sum_host) (void)hipHostFree(c->sum_host);
+  if (c->head_h) (void)hipHostFree(c->head_h);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -350,6 +352,9 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
 static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
                           npr_endianness e, int speculative_start, uint64_t ref_record, const npr_dev_outputs *o,
                           uint64_t chunk_bytes, void *stream, const ShardSpec *sh);
+static npr_status range_params(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                               npr_endianness e, int speculative_start, uint64_t ref_record, const ShardSpec *sh,
+                               npr::ParseParams &p, uint64_t &nt);
 
 npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness e, int speculative_start,
@@ -382,7 +387,33 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
     return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream, sh);
   npr_status st = res_geometry(c);
   if (st) return st;
-  const uint64_t chunk = chunk_bytes ? chunk_bytes : (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
+  uint64_t chunk = chunk_bytes;
+  if (!chunk) {  // one launch keeps kResSlots rounds of 64 records per wave in registers
+    const uint64_t dense = (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;  // >= 64 records per tile
+    chunk = dense;
+    if (stop - start >= 8 * dense && !speculative_start && !sh) {
+      // large: size the links by the record density of the capture's first 256 KiB, walked here from
+      // the known first record (one small D2H copy and a sync; results never depend on it)
+      constexpr uint64_t kHead = 256u << 10;
+      const uint64_t nb = std::min<uint64_t>(stop - start, kHead);
+      if (!c->head_h) HIP_CHECK(c, hipHostMalloc((void **)&c->head_h, kHead, 0));
+      const uint8_t *head = c->head_h;
+      hipStream_t s = pick(c, stream);
+      HIP_CHECK(c, hipMemcpyAsync(c->head_h, (const uint8_t *)input + start, nb, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(c, hipStreamSynchronize(s));
+      uint64_t off = 0, n = 0;
+      while (off + 16 <= nb) {
+        const uint32_t incl = rd_u32(head + off + 8, e == NPR_BIG);
+        if (off + 16 + incl > nb) break;
+        off += 16 + (uint64_t)incl;
+        ++n;
+      }
+      if (n >= 64) {  // 3/4 of the kept capacity at that many bytes per record
+        const uint64_t fit = (uint64_t)c->res_waves * npr::kResSlots * 64 * 3 / 4 * (off / n);
+        chunk = std::max(dense, fit);
+      }
+    }
+  }
   if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
   npr_dev_outputs oc = *o;
   const npr_summary *prev = nullptr;
@@ -414,36 +445,22 @@ npr_status npr_dev_parse_extract_shard(npr_ctx *c, const void *input, uint64_t i
                  shard->chunk_bytes, stream, &sh);
 }
 
-static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
-                               npr_endianness e, int speculative_start, uint64_t ref_record,
-                               const npr_summary *prev, const npr_dev_outputs *o, void *stream,
-                               const ShardSpec *sh) {
-  if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
-  if (stop > len || start > stop) return fail(c, NPR_ERR_ARG, "need start <= stop <= len");
-  if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
-  if (o->flows && (((uintptr_t)o->flows & 15u) != 0 || (o->flows_v6 && ((uintptr_t)o->flows_v6 & 15u))))
-    return fail(c, NPR_ERR_ARG, "flow arrays must be 16-byte aligned");
-  if (len >= (1ull << 40)) return fail(c, NPR_ERR_ARG, "input larger than 1 TiB (40-bit record offsets)");
-  HIP_CHECK(c, hipSetDevice(c->device));
+// The range-dependent launch parameters of records starting in [start, stop) (no workspace).
+static npr_status range_params(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                               npr_endianness e, int speculative_start, uint64_t ref_record, const ShardSpec *sh,
+                               npr::ParseParams &p, uint64_t &nt) {
   const uint64_t base = sh ? sh->base : 0;
   if (start < base) return fail(c, NPR_ERR_ARG, "need start >= base");
   uint64_t org = 0;
-  const uint64_t nt = tiles_for(stop - base, start - base, &org);  // tiles cover [org, stop)
+  nt = tiles_for(stop - base, start - base, &org);  // tiles cover [org, stop)
   org += base;
   if (nt > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large");
-  npr_status st = ensure(c, c->slots, slot_bytes(nt), true);
-  if (st) return st;
-  if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
-  hipStream_t s = pick(c, stream);
-  if ((st = next_epoch(c, s))) return st;
-  npr::ParseParams p{};
   p.buf = (const uint8_t *)input - base;  // buf + o = file byte o (only o >= base is ever read)
   p.base = base;
   p.len = len;
   p.start = start;
   p.org = org;
   p.big = e == NPR_BIG;
-  p.epoch = c->epoch;
   p.ntiles = (uint32_t)nt;
   p.frac_max = 1000000000u;
   p.stop = stop;
@@ -457,6 +474,29 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.ts_ref = sh->ts_ref;
     p.ref = ~0ull;
   }
+  return NPR_OK;
+}
+
+static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
+                               npr_endianness e, int speculative_start, uint64_t ref_record,
+                               const npr_summary *prev, const npr_dev_outputs *o, void *stream,
+                               const ShardSpec *sh) {
+  if (!c || !o || !o->summary || (!input && len)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (stop > len || start > stop) return fail(c, NPR_ERR_ARG, "need start <= stop <= len");
+  if (((uintptr_t)input & 15u) != 0) return fail(c, NPR_ERR_ARG, "input must be 16-byte aligned");
+  if (o->flows && (((uintptr_t)o->flows & 15u) != 0 || (o->flows_v6 && ((uintptr_t)o->flows_v6 & 15u))))
+    return fail(c, NPR_ERR_ARG, "flow arrays must be 16-byte aligned");
+  if (len >= (1ull << 40)) return fail(c, NPR_ERR_ARG, "input larger than 1 TiB (40-bit record offsets)");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr::ParseParams p{};
+  uint64_t nt = 0;
+  npr_status st = range_params(c, input, len, start, stop, e, speculative_start, ref_record, sh, p, nt);
+  if (st) return st;
+  if ((st = ensure(c, c->slots, slot_bytes(nt), true))) return st;
+  if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
+  hipStream_t s = pick(c, stream);
+  if ((st = next_epoch(c, s))) return st;
+  p.epoch = c->epoch;
   p.timeout_ticks = kTimeoutTicks;
   p.slots = (npr::TileSlot *)c->slots.p;
   uint64_t nl[npr::kLevels + 1];

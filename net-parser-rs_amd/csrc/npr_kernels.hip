@@ -1344,11 +1344,31 @@ __device__ __forceinline__ uint32_t res_wave_of(const ParseParams &kp, int64_t m
   const uint64_t big = (uint64_t)r * (q + 1);
   return (uint64_t)m < big ? (uint32_t)((uint64_t)m / (q + 1)) : (uint32_t)(r + ((uint64_t)m - big) / q);
 }
+// L2 prefetch beyond the LDS ring: one LDS-DMA of a dword from every 128-B line of the tile into
+// a junk LDS word per lane (an LDS destination, so no VGPR is written behind the compiler's back;
+// bytes past the range are out of the descriptor and fetch nothing).  The ring's DMA of the tile,
+// kPfAhead iterations later, then hits the XCD's L2 instead of waiting out an HBM round trip: a
+// sparse capture's tile is walked in far less time than that latency.
+#ifndef NPR_PF_AHEAD
+#define NPR_PF_AHEAD 0
+#endif
+constexpr int kPfAhead = NPR_PF_AHEAD;  // tiles prefetched beyond the ring (0, the default: measured slower at C2 and C3)
+constexpr int kPfAfter = kPfAhead ? (kResRing < kPfAhead + 1 ? kResRing : kPfAhead + 1) : 0;  // PFs after any DMA
+__device__ __forceinline__ void pf_tile(const ParseParams &kp, uint64_t tile_lo, uint64_t hi, uint32_t *junk) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t avail = hi > tile_lo ? hi - tile_lo : 0;
+  const uint32_t nbytes = avail < (uint64_t)kTile ? (uint32_t)avail : (uint32_t)kTile;
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + (avail ? tile_lo : 0)), 0, (int)nbytes, 0x00020000);
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)junk, 4, lane * 128u, 0, 0, 0);
+}
 // wait until at most `ahead` tiles' DMAs are outstanding (the youngest vector-memory
-// instructions are always the DMAs of the tiles ahead, so this retires the current tile)
+// instructions are the DMAs of the tiles ahead and at least PF prefetches, so this retires the
+// current tile)
+template <int PF>
 __device__ __forceinline__ void res_wait(uint32_t ahead) {
-  constexpr int w1 = kDmaPer, w2 = 2 * kDmaPer;
-  if (ahead == 0) __builtin_amdgcn_s_waitcnt(0x0F70);
+  constexpr int w0 = PF, w1 = kDmaPer + PF, w2 = 2 * kDmaPer + PF;
+  if (ahead == 0) __builtin_amdgcn_s_waitcnt(0x0F70 | (w0 & 15) | ((w0 >> 4) << 14));
   else if (ahead == 1 || kResRing <= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (w1 & 15) | ((w1 >> 4) << 14));
   else __builtin_amdgcn_s_waitcnt(0x0F70 | (w2 & 15) | ((w2 >> 4) << 14));
   wave_sync();
@@ -1619,7 +1639,7 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     if (t + kResRing - 1 < c1)
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.data[(slot + kResRing - 1) % kResRing]);
-    res_wait(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    res_wait<0>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
     const uint32_t *w = sh.data[slot];
     if (!ended && pos >= tile_lo && pos < tile_hi) {
       uint32_t n = 0;
@@ -1657,6 +1677,8 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
 
 struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS fold
   ResShared w[kResWg];
+  uint32_t junk[64];  // L2-prefetch destinations (every wave's, overwritten freely)
+  uint32_t prog[kResWg];  // tiles each wave has parsed in phase A (~0: done or inactive), for fair priorities
   Seg a[kResWg];   // each wave's range aggregate A
   Seg x[kResWg];   // each wave's prefix: anchor ⊕ G(0..b-1) ⊕ A(waves before it here)
   uint32_t fail;   // a bounded wait of wave 0 timed out: every wave leaves
@@ -1678,10 +1700,14 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
   const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;  // chained: tile 0 speculates too
   if (threadIdx.x == 0) sh.fail = 0;
+  if (lane == 0) sh.prog[wid] = active && c0 < c1 ? 0u : ~0u;
   const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
 #pragma unroll
   for (int k = 0; k < kResRing - 1; ++k)
     if (c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
+  const uint64_t range_end = kp.org + (uint64_t)c1 * kTile < kp.len ? kp.org + (uint64_t)c1 * kTile : kp.len;
+#pragma unroll
+  for (int k = 0; k < kPfAhead; ++k) pf_tile(kp, base + (uint64_t)(kResRing - 1 + k) * kTile, range_end, sh.junk);
 #ifndef NPR_EXP_NOPRIO
   __builtin_amdgcn_s_setprio(3);  // lowered by one per tile parsed (below)
 #endif
@@ -1690,6 +1716,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   uint32_t fl[kResSlots][8];                   // kept rounds: d[0..6] (IPv6: d[0] = address offset), record offset - base
   uint32_t m_ok = 0, m_lo = 0, m_hi = 0;       // lane k: Ok flows before kept round k, its Ok ballot
   uint32_t ns = 0;                             // kept rounds
+  uint32_t fill = 64;                          // lanes used in kept round ns - 1
   uint64_t entry = kNone, pos = kNone;         // speculated entry; chain position
   bool ended = false;
   uint32_t cnt = 0, okc = 0;                   // records / Ok flows of the range (speculative chain)
@@ -1703,7 +1730,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
     if (t + kResRing - 1 < c1)
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
-    res_wait(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    if (kPfAhead) pf_tile(kp, tile_lo + (uint64_t)(kResRing - 1 + kPfAhead) * kTile, range_end, sh.junk);
+    res_wait<kPfAfter>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
     if (t == c0) {
       sc = spec_ctx(kp, scb);
       if (DIAG) stamp_at(st, 1);
@@ -1726,35 +1754,49 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n));
         wave_sync();
         const uint32_t rounds = (n + 63u) >> 6;
-        if (tdef == c1 && ns + rounds > (uint32_t)kResSlots) {  // out of registers: defer the rest
+        // a tile of few records (sparse captures) shares the last kept round when it fits there
+        const bool pack = ns > 0 && fill + n <= 64u && n > 0;
+        if (tdef == c1 && ns + (pack ? 0u : rounds) > (uint32_t)kResSlots) {  // out of registers: defer the rest
           tdef = t;
           pdef = pos;
           cdef = cnt;
           odef = okc;
         }
         if (tdef == c1) {
-          for (uint32_t s = 0; s < rounds; ++s) {
-            const uint32_t i = lane + s * 64u;
-            const bool valid = i < n;
+          // fresh rounds: lane l of round s decodes record 64 s + l; packed (one round): lane
+          // fill + i decodes record i, so its flow lands in its lane of round ns - 1 directly
+          const uint32_t nr = pack ? 1u : rounds;
+          const uint32_t fu = pack ? __builtin_amdgcn_readfirstlane(fill) : 0u;
+          for (uint32_t s = 0; s < nr; ++s) {
+            const uint32_t qu = __builtin_amdgcn_readfirstlane(pack ? ns - 1u : ns);  // uniform: one scalar branch per slot
+            const uint32_t i = pack ? ((lane - fu) & 63u) : lane + s * 64u;
+            const bool valid = pack ? (lane >= fu && lane < fu + n) : i < n;
             FlowWords f;
             const uint32_t rel = sh.w[wid].srec[i];
+#ifdef NPR_EXP_NODECODE  // ablation (timing only: wrong flow fields)
+            f = FlowWords{};
+            const bool okr = valid;
+#else
             const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
+#endif
             const uint64_t bal = __ballot(okr);
             const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
                                     f.d[4], f.d[5], f.d[6], (uint32_t)(tile_lo + rel - base)};
-            const uint32_t nsu = __builtin_amdgcn_readfirstlane(ns);  // uniform: one scalar branch per slot
+            const bool keep = pack && !valid;  // packed: the round's earlier lanes stay
 #pragma unroll
             for (int q = 0; q < kResSlots; ++q)
-              if ((uint32_t)q == nsu) {
+              if ((uint32_t)q == qu) {
 #pragma unroll
-                for (int j = 0; j < 8; ++j) fl[q][j] = sw[j];
+                for (int j = 0; j < 8; ++j) fl[q][j] = keep ? fl[q][j] : sw[j];
               }
-            m_ok = lane == ns ? okc : m_ok;
-            m_lo = lane == ns ? (uint32_t)bal : m_lo;
-            m_hi = lane == ns ? (uint32_t)(bal >> 32) : m_hi;
-            ++ns;
+            m_ok = lane == qu && !pack ? okc : m_ok;
+            m_lo = lane == qu ? (pack ? m_lo : 0u) | (uint32_t)bal : m_lo;
+            m_hi = lane == qu ? (pack ? m_hi : 0u) | (uint32_t)(bal >> 32) : m_hi;
+            if (!pack) ++ns;
             okc += (uint32_t)__builtin_popcountll(bal);
           }
+          if (pack) fill = fu + n;
+          else if (rounds) fill = n - 64u * (rounds - 1u);  // lanes used in the last kept round
         } else {  // deferred: status only (the Ok count), flows re-read in phase B
           for (uint32_t s = 0; s < rounds; ++s) {
             const uint32_t i = lane + s * 64u;
@@ -1771,13 +1813,26 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     }
     wave_sync();  // done with this slot before it is refilled
 #ifndef NPR_EXP_NOPRIO
-    // keep the CU's 16 waves in step: the SIMD arbiter favours older waves, which would finish
-    // their ranges several us before the younger ones (and the workgroup waits for its last)
-    if (k == 0) __builtin_amdgcn_s_setprio(2);
-    else if (k == 1) __builtin_amdgcn_s_setprio(1);
-    else if (k == 2) __builtin_amdgcn_s_setprio(0);
+    // keep the CU's waves in step: the SIMD arbiter favours older waves, which would finish their
+    // ranges long before the younger ones (C3: the four age ranks of a SIMD finished phase A at
+    // 125 / 139 / 157 / 179 us), and the workgroup waits for its last.  Each tile, a wave d tiles
+    // ahead of the workgroup's slowest runs at priority 3 - min(d, 3).
+    {
+      if (lane == 0) sh.prog[wid] = k + 1;
+      uint32_t mn = lane < kResWg ? sh.prog[lane] : ~0u;
+#pragma unroll
+      for (int o = 1; o < (int)kResWg; o <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+      const uint32_t d = k + 1 - __builtin_amdgcn_readfirstlane(mn);
+      if (d == 0) __builtin_amdgcn_s_setprio(3);
+      else if (d == 1) __builtin_amdgcn_s_setprio(2);
+      else if (d == 2) __builtin_amdgcn_s_setprio(1);
+      else __builtin_amdgcn_s_setprio(0);
+    }
 #endif
   }
+#ifndef NPR_EXP_NOPRIO
+  if (lane == 0) sh.prog[wid] = ~0u;  // done: no longer the slowest
+#endif
   if (DIAG) stamp_at(st, 2);
   const uint32_t ep = kp.epoch;
   if (active && lane == 0) {  // A: in LDS for the workgroup fold, in HBM for the rare generic prefix
