@@ -1,9 +1,9 @@
-// stream_probe — what streaming pattern reaches HBM bandwidth on this MI355X (no parsing at all).
+// dma_ring — what streaming pattern reaches HBM bandwidth on this MI355X (no parsing at all).
 // Every variant reads a 1 GiB buffer once; W persistent waves each own a contiguous range, as
 // k_parse_resident's phase A does.  Prints GB/s per variant.
 //   reg   : global_load_dwordx4 to registers, K loads per lane in flight
 //   dma R : buffer_load_dwordx4 ... lds into an R-slot ring of 4 KiB tiles per wave (R-1 in flight)
-// Build: hipcc -O3 --offload-arch=gfx950 scripts/stream_probe.hip -o scripts/stream_probe
+// Build: hipcc -O3 --offload-arch=gfx950 scripts/microbench/dma_ring.hip -o scripts/microbench/dma_ring
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
