@@ -812,8 +812,12 @@ __device__ __forceinline__ int stride_grade(const SpecCtx &c, const uint32_t *w,
 // Stride speculation: while the record length repeats, lane j confirms records j, j+64, j+128,
 // j+192 ahead in one LDS round trip (up to 256 records per step); one record per step otherwise.
 constexpr int kWalkUnroll = 4;
+// last_io: the incl_len of the record before `entry` (in), of the last record walked (out), so a
+// wave walking consecutive tiles keeps hopping through variable-length traffic; NULL: unknown
+// (the first record tries a stride)
+constexpr uint32_t kAnyLen = ~0u;  // walk_tile: no previous record length known
 __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
-                              uint64_t tile_hi, uint64_t entry, uint32_t &n_out) {
+                              uint64_t tile_hi, uint64_t entry, uint32_t &n_out, uint32_t *last_io = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const bool big = kp.big;
   const uint32_t span = (uint32_t)(tile_hi - tile_lo);
@@ -821,15 +825,21 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
   const uint32_t avail = av > 0xffffffffull ? 0xffffffffu : (uint32_t)av;  // bytes from tile_lo
   uint64_t p = uni64(entry);
   uint32_t n = 0;
+  uint32_t last = last_io ? *last_io : kAnyLen;  // the previous record's incl_len
   while (p < tile_hi) {
     const uint32_t r = (uint32_t)(p - tile_lo);
     // wave-uniform (one address): readfirstlane keeps the chain position scalar
     const uint32_t incl = __builtin_amdgcn_readfirstlane(hdr(w, r, 2, big));
+    if (last == kAnyLen) last = incl;
     if (kp.len - p < 16 || kp.len - p - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
-    if (incl > (uint32_t)kTile) {  // a record longer than a tile: no stride to speculate on
+    // a record longer than a tile (no stride to speculate on), or one whose length differs from
+    // the previous record's (variable-length traffic: a stride guess would confirm only itself):
+    // one hop, one header read
+    if (incl > (uint32_t)kTile || incl != last) {
       if (lane == 0) srec[n] = (uint16_t)r;
       n += 1;
       p += 16ull + incl;
+      last = incl;
       continue;
     }
     const uint32_t stride = 16u + incl;
@@ -869,8 +879,10 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
     for (int u = 0; u < kWalkUnroll; ++u) srec[n + lane + 64u * (uint32_t)u] = (uint16_t)qr[u];
     n += m;
     p += (uint64_t)m * stride;
+    last = incl;
   }
   n_out = n;
+  if (last_io) *last_io = last;
   return p;
 }
 
@@ -1633,6 +1645,7 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
   for (int k = 0; k < kResRing - 1; ++k)
     if (t_from + k < c1) dma_tile<2>(kp, kp.org + (uint64_t)(t_from + k) * kTile, sh.data[k]);
   bool ended = false;
+  uint32_t wlast = kAnyLen;
   for (uint32_t t = t_from; t < c1; ++t) {
     const uint32_t slot = (t - t_from) % kResRing;
     const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
@@ -1643,7 +1656,7 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
     const uint32_t *w = sh.data[slot];
     if (!ended && pos >= tile_lo && pos < tile_hi) {
       uint32_t n = 0;
-      const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n));
+      const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n, &wlast));
       wave_sync();
       uint32_t okbase = 0;
       for (int s = 0; s < kRounds; ++s) {
@@ -1724,6 +1737,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   uint64_t pdef = 0;
   uint32_t cdef = 0, odef = 0;
   SpecCtx sc{};
+  uint32_t wlast = kAnyLen;  // incl_len of the last record walked (walk_tile)
+  uint64_t wait_ticks = 0;  // DIAG: phase A time spent waiting for tiles to land
   for (uint32_t t = c0; t < c1; ++t) {
     const uint32_t k = t - c0, slot = k % kResRing;
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
@@ -1731,7 +1746,9 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     if (t + kResRing - 1 < c1)
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
     if (kPfAhead) pf_tile(kp, tile_lo + (uint64_t)(kResRing - 1 + kPfAhead) * kTile, range_end, sh.junk);
+    const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     res_wait<kPfAfter>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    if (DIAG) wait_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
     if (t == c0) {
       sc = spec_ctx(kp, scb);
       if (DIAG) stamp_at(st, 1);
@@ -1751,7 +1768,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       }
       if (pos != kNone && pos < tile_hi) {
         uint32_t n = 0;
-        const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n));
+        const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n, &wlast));
         wave_sync();
         const uint32_t rounds = (n + 63u) >> 6;
         // a tile of few records (sparse captures) shares the last kept round when it fits there
@@ -2018,7 +2035,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     st.v[9] = ns;
     st.v[10] = c1 - tdef;
     st.v[11] = (entry != kNone && xe == pos) ? 1 : 0;
-    stamp_flush(kp, st, v, wid == 0 ? 0x7F7Fu : 0xF7Fu);
+    st.v[15] = wait_ticks;
+    stamp_flush(kp, st, v, wid == 0 ? 0xFF7Fu : 0x8F7Fu);
   }
 }
 
