@@ -39,6 +39,7 @@ struct npr_ctx {
   int resident = 1;        // NPR_OPT_RESIDENT
   uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
   uint32_t pipe_waves = 0; // ... of the pipelined resident pass (a multiple of 15)
+  bool res_pack = false;   // chained(): its links pack sparse tiles into kept rounds
   int pipe = 0;            // NPR_OPT_PIPE: 1 = flows-only launches run k_parse_pipe (0: k_parse_resident)
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
   const npr_summary *sum_ptr[2] = {nullptr, nullptr};  // summaries the last two launches wrote
@@ -388,6 +389,7 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
   npr_status st = res_geometry(c);
   if (st) return st;
   uint64_t chunk = chunk_bytes;
+  bool pack = chunk_bytes > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
   if (!chunk) {  // one launch keeps kResSlots rounds of 64 records per wave in registers
     const uint64_t dense = (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;  // >= 64 records per tile
     chunk = dense;
@@ -412,9 +414,15 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
         const uint64_t fit = (uint64_t)c->res_waves * npr::kResSlots * 64 * 3 / 4 * (off / n);
         chunk = std::max(dense, fit);
       }
+      pack = chunk > dense;  // links past one kept round per tile: sparse tiles must share rounds
     }
   }
   if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
+  struct PackScope {  // this call's links run the packing resident pass; later launches do not
+    npr_ctx *c;
+    ~PackScope() { c->res_pack = false; }
+  } pack_scope{c};
+  c->res_pack = pack;
   npr_dev_outputs oc = *o;
   const npr_summary *prev = nullptr;
   uint64_t lo = start;
@@ -565,6 +573,7 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.nwaves = (uint32_t)wv;
     p.rslots = (npr::RangeSlot *)c->slots.p;
     p.rgroups = p.groups[1];
+    p.pack = c->res_pack ? 1u : 0u;
     // every workgroup aggregate the launch writes must lie inside the slot allocation
     const uint64_t nb = (wv + npr::kResWgMin - 1) / npr::kResWgMin;
     if ((const char *)(p.rgroups + nb) > (const char *)c->slots.p + c->slots.cap)

@@ -121,6 +121,7 @@ struct ParseParams {
   uint32_t pipe;           // 1: the pipelined resident pass (k_parse_pipe): nwaves = parser waves (15 per
                            //    workgroup), tile t = round * nwaves + parser, rslots[t] per TILE,
                            //    rgroups[t / 15] per workgroup round
+  uint32_t pack;           // resident pass: sparse tiles share kept rounds (k_parse_resident<.., true>)
   const npr_summary *prev; // chained launch (resident pass only): continue the chain and the counts
   uint32_t prev_epoch;     //   of the launch that wrote *prev (its epoch, 0 = unchecked); NULL = none
 };

@@ -1365,6 +1365,7 @@ __device__ __forceinline__ uint32_t res_wave_of(const ParseParams &kp, int64_t m
 #define NPR_PF_AHEAD 0
 #endif
 constexpr int kPfAhead = NPR_PF_AHEAD;  // tiles prefetched beyond the ring (0, the default: measured slower at C2 and C3)
+constexpr uint32_t kStepPrioTiles = 8;  // wave ranges up to this many tiles use stepped priorities
 constexpr int kPfAfter = kPfAhead ? (kResRing < kPfAhead + 1 ? kResRing : kPfAhead + 1) : 0;  // PFs after any DMA
 __device__ __forceinline__ void pf_tile(const ParseParams &kp, uint64_t tile_lo, uint64_t hi, uint32_t *junk) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -1697,7 +1698,9 @@ struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS 
   uint32_t fail;   // a bounded wait of wave 0 timed out: every wave leaves
 };
 
-template <bool DIAG>
+// PACK: sparse tiles share kept rounds (links sized past one round per tile; the host sets it from
+// the capture's density).  A separate instantiation: the merge costs dense captures registers.
+template <bool DIAG, bool PACK>
 __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams kp) {
   __shared__ __attribute__((aligned(16))) ResWgShared sh;
   const uint32_t lane = threadIdx.x & 63u;
@@ -1772,7 +1775,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         wave_sync();
         const uint32_t rounds = (n + 63u) >> 6;
         // a tile of few records (sparse captures) shares the last kept round when it fits there
-        const bool pack = ns > 0 && fill + n <= 64u && n > 0;
+        const bool pack = PACK && ns > 0 && fill + n <= 64u && n > 0;
         if (tdef == c1 && ns + (pack ? 0u : rounds) > (uint32_t)kResSlots) {  // out of registers: defer the rest
           tdef = t;
           pdef = pos;
@@ -1832,9 +1835,15 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
 #ifndef NPR_EXP_NOPRIO
     // keep the CU's waves in step: the SIMD arbiter favours older waves, which would finish their
     // ranges long before the younger ones (C3: the four age ranks of a SIMD finished phase A at
-    // 125 / 139 / 157 / 179 us), and the workgroup waits for its last.  Each tile, a wave d tiles
-    // ahead of the workgroup's slowest runs at priority 3 - min(d, 3).
-    {
+    // 125 / 139 / 157 / 179 us), and the workgroup waits for its last.  Long ranges: each tile, a
+    // wave d tiles ahead of the workgroup's slowest runs at priority 3 - min(d, 3) (C3 link
+    // 258 -> 222 us); short ones (C2: 4-5 tiles) step down per tile, which costs less there
+    // (33.2 vs 34.1 us).
+    if (c1 - c0 <= kStepPrioTiles) {  // short ranges: step down after each of the first three tiles
+      if (k == 0) __builtin_amdgcn_s_setprio(2);
+      else if (k == 1) __builtin_amdgcn_s_setprio(1);
+      else if (k == 2) __builtin_amdgcn_s_setprio(0);
+    } else {
       if (lane == 0) sh.prog[wid] = k + 1;
       uint32_t mn = lane < kResWg ? sh.prog[lane] : ~0u;
 #pragma unroll
@@ -2052,7 +2061,7 @@ int pipe_waves_per_cu() {
 
 int resident_waves_per_cu() {
   int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false>), kResWg * kWave, 0) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false, false>), kResWg * kWave, 0) !=
       hipSuccess)
     return 0;
   return nb * (int)kResWg;
@@ -2076,8 +2085,10 @@ hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
   }
   if (p.nwaves) {
     const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
-    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_resident<true>), dim3(nb), dim3(kResWg * kWave), 0, s, p);
-    else hipLaunchKernelGGL((k_parse_resident<false>), dim3(nb), dim3(kResWg * kWave), 0, s, p);
+    const bool diag = p.stats || p.stamps;
+    auto k = diag ? (p.pack ? k_parse_resident<true, true> : k_parse_resident<true, false>)
+                  : (p.pack ? k_parse_resident<false, true> : k_parse_resident<false, false>);
+    hipLaunchKernelGGL(k, dim3(nb), dim3(kResWg * kWave), 0, s, p);
     return hipGetLastError();
   }
   return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
