@@ -133,6 +133,18 @@ typedef enum npr_flow_status {
   NPR_FLOW_STATUS_COUNT = 25
 } npr_flow_status;
 
+/* VXLAN inner flows (row f3; off the reference's flow path, which never produces a Vxlan flow,
+ * quirk Q13): the outer frame's UDP payload parsed as Vxlan::parse (src/layer4/vxlan.rs:31-48),
+ * then the inner Ethernet frame's flow as <Vxlan as FlowExtraction>::extract_flow
+ * (src/flow/layer4/vxlan.rs:32-50).  Per-record status: an outer failure keeps its
+ * npr_flow_status code (1..24); then: */
+enum {
+  NPR_VXLAN_NOT_UDP = 32,    /* the outer flow is Ok but TCP */
+  NPR_VXLAN_PORT = 33,       /* the outer UDP destination port is not the one asked for */
+  NPR_VXLAN_INCOMPLETE = 34, /* the UDP payload is shorter than the 8-B VXLAN header (Incomplete) */
+  NPR_VXLAN_INNER = 64       /* + the inner frame's npr_flow_status (1..24): the inner flow failed */
+};
+
 /* Totals written by the device at the end of a parse.  `consumed` is where the record
  * chain stopped: the Rust remainder slice is input[consumed..] (src/record.rs:51). */
 typedef struct npr_summary {
@@ -346,6 +358,10 @@ npr_status npr_dev_parse_extract_shard(npr_ctx *ctx, const void *input, uint64_t
 /* Synchronise `stream`, copy the summary back and map its flags to a status. */
 npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
                          npr_summary *host_summary);
+/* Host-memory form of npr_dev_vxlan_flows (synchronous). */
+npr_status npr_vxlan_flows(npr_ctx *ctx, const uint8_t *input, size_t len, const npr_record *records, size_t n,
+                           uint32_t dst_port, npr_endianness endianness, npr_flow *flows, npr_flow_v6 *flows_v6,
+                           uint8_t *status, uint32_t *vni);
 /* Dense extract_flow over device-resident records (device npr_record array indexing into
  * `input`; payload = input[offset+16 .. offset+16+actual_length]). */
 npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
@@ -355,6 +371,16 @@ npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
  * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
  * cap are not written), *n_out (a device word) = the number of Ok flows, or UINT64_MAX when the
  * launch's bounded look-back timed out.  One kernel pass. */
+/* VXLAN inner flows of device-resident records (row f3): dense outputs, row i for record i.
+ * flows[i] = the INNER frame's flow with records[i]'s offset when status[i] == NPR_FLOW_OK
+ * (zero row otherwise), flows_v6[i] its IPv6 addresses, vni[i] = the VXLAN network identifier
+ * (raw u32 >> 8, src/layer4/vxlan.rs:44) when the header was read, else 0.  dst_port = 0 takes
+ * every outer UDP flow, else only that destination port (4789 is the IANA VXLAN port).
+ * `endianness` is Vxlan::parse's (the reference's tests pass NPR_BIG, src/layer4/vxlan.rs:91).
+ * Any output array may be NULL. */
+npr_status npr_dev_vxlan_flows(npr_ctx *ctx, const void *input, uint64_t len, const npr_record *records,
+                               uint64_t n, uint32_t dst_port, npr_endianness endianness, npr_flow *flows,
+                               npr_flow_v6 *flows_v6, uint8_t *status, uint32_t *vni, void *stream);
 npr_status npr_dev_convert_records(npr_ctx *ctx, const void *input, uint64_t len,
                                    const npr_record *records, uint64_t n, npr_flow *out,
                                    npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream);

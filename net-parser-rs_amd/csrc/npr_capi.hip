@@ -613,6 +613,17 @@ static npr_status convert_launch(npr_ctx *c, const void *input, uint64_t len, co
   return NPR_OK;
 }
 
+npr_status npr_dev_vxlan_flows(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
+                               uint32_t dst_port, npr_endianness e, npr_flow *flows, npr_flow_v6 *flows_v6,
+                               uint8_t *status, uint32_t *vni, void *stream) {
+  if (!c || (!input && len) || (!recs && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (dst_port > 0xffffu) return fail(c, NPR_ERR_ARG, "dst_port must be 0..65535");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  HIP_CHECK(c, npr::launch_vxlan_flows((const uint8_t *)input, len, recs, n, dst_port, e == NPR_BIG, (uint32_t *)flows,
+                                       (uint32_t *)flows_v6, status, vni, pick(c, stream)));
+  return NPR_OK;
+}
+
 npr_status npr_dev_convert_records(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
                                    npr_flow *out, npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream) {
   if (!c || (!input && len) || (!recs && n) || !n_out || (!out && cap)) return fail(c, NPR_ERR_ARG, "null argument");
@@ -966,6 +977,33 @@ npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const np
   if (flows_v6)
     HIP_CHECK(c, hipMemcpyAsync(flows_v6, c->flows_v6.p, n * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
   if (status) HIP_CHECK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  return NPR_OK;
+}
+
+npr_status npr_vxlan_flows(npr_ctx *c, const uint8_t *in, size_t len, const npr_record *records, size_t n,
+                           uint32_t dst_port, npr_endianness e, npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status,
+                           uint32_t *vni) {
+  if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (dst_port > 0xffffu) return fail(c, NPR_ERR_ARG, "dst_port must be 0..65535");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = stage_input(c, in, len);
+  if (st) return st;
+  if (n == 0) return NPR_OK;
+  if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
+  if ((st = ensure(c, c->flows, n * sizeof(npr_flow)))) return st;
+  if ((st = ensure(c, c->flows_v6, n * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->status, n))) return st;
+  if ((st = ensure(c, c->flows2, n * sizeof(uint32_t)))) return st;  // the VNIs
+  HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, npr::launch_vxlan_flows((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n, dst_port,
+                                       e == NPR_BIG, (uint32_t *)c->flows.p, (uint32_t *)c->flows_v6.p,
+                                       (uint8_t *)c->status.p, (uint32_t *)c->flows2.p, c->stream));
+  if (flows) HIP_CHECK(c, hipMemcpyAsync(flows, c->flows.p, n * sizeof(npr_flow), hipMemcpyDeviceToHost, c->stream));
+  if (flows_v6)
+    HIP_CHECK(c, hipMemcpyAsync(flows_v6, c->flows_v6.p, n * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
+  if (status) HIP_CHECK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  if (vni) HIP_CHECK(c, hipMemcpyAsync(vni, c->flows2.p, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   return NPR_OK;
 }

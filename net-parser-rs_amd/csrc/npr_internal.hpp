@@ -136,6 +136,10 @@ constexpr uint32_t kPipeGroupTiles = 15;  // tiles per group slot of the pipelin
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);
+// row f3: VXLAN inner flows (dense, row i for record i; any output may be NULL)
+hipError_t launch_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint32_t dst_port,
+                              bool big, uint32_t *flows, uint32_t *flows_v6, uint8_t *status, uint32_t *vni,
+                              hipStream_t s);
 // convert_records in one pass (k_convert_records): rows 0.. = Ok flows in reverse record order,
 // *total = all Ok flows (rows past cap are not written; ~0 when a bounded wait timed out).
 // look: convert_look_words(n) granules whose tags are not `epoch` at launch.

@@ -109,6 +109,7 @@ struct FlowWords {
   uint32_t d[7];
   uint32_t v6[8];
   uint32_t v6off;  // payload offset of the IPv6 address block (the resident kernel re-reads it)
+  uint32_t l4off;  // payload offset of the L4 header (decode<> only; the VXLAN path reads past it)
 };
 
 // InternetProtocolId::new (src/layer3/mod.rs:54-72)
@@ -249,6 +250,7 @@ __device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f)
     return v6 ? NPR_FLOW_L3_IPV6_PROTOCOL : NPR_FLOW_L3_IPV4_PROTOCOL;
   }
   if (FIELDS) {  // Flow::new (src/flow/mod.rs:64-86)
+    f.l4off = l4;
     const uint32_t wp = r.le32(l4);
     f.d[2] = be16_of(wp) | (be16_of(wp >> 16) << 16);
     f.d[3] = vlan | (m1 & 0xffff0000u);
@@ -2235,6 +2237,84 @@ hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_reco
   const uint64_t blocks = (n + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_extract_dense, dim3((uint32_t)blocks), dim3(kBlock), 0, s, buf, len, recs, n,
                      flows, flows_v6, status);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// row f3: VXLAN inner flows over caller-supplied records.  One lane per record, bytes read
+// through GlobalReader (an off-path decoder: the general decode<> twice, outer then inner).
+//   outer: FlowExtraction::extract_flow of the record; Ok and UDP (to dst_port unless 0);
+//   Vxlan::parse(udp payload, endianness) (src/layer4/vxlan.rs:31-48): flags, group policy id,
+//     raw network identifier (u16, u16, u32), payload = rest -> Incomplete below 8 bytes;
+//   <Vxlan as FlowExtraction>::extract_flow (src/flow/layer4/vxlan.rs:32-50): the inner
+//     Ethernet frame's flow (its remainder is always empty).
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record *recs,
+                                                        uint64_t n, uint32_t dst_port, uint32_t big,
+                                                        uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
+                                                        uint32_t *vni_out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  const npr_record rc = load_record(recs, i);
+  const uint64_t off = rc.offset + 16;
+  uint32_t st = 0xffu, vni = 0;  // 0xff: the record does not lie inside the buffer
+  FlowWords f{};
+  if (off <= len && len - off >= rc.actual_length) {
+    const GlobalReader r{buf + off, len - off};
+    st = decode<true>(r, rc.actual_length, f);
+    if (st == NPR_FLOW_OK) {
+      if (!(f.d[6] & (NPR_FLOW_KIND_UDP << 16))) {
+        st = NPR_VXLAN_NOT_UDP;
+      } else if (dst_port && (f.d[2] >> 16) != dst_port) {
+        st = NPR_VXLAN_PORT;
+      } else {
+        // an Ok UDP flow: payload = [l4 + 8, l4 + L) with L the UDP length (== the IP payload)
+        const uint32_t L = be16_of(r.le32(f.l4off + 4u));
+        const uint32_t po = f.l4off + 8u, pl = L - 8u;
+        if (pl < 8u) {
+          st = NPR_VXLAN_INCOMPLETE;
+        } else {
+          const uint32_t w = r.le32(po + 4u);
+          const uint32_t raw = big ? __builtin_bswap32(w) : w;  // u32!(endianness) (:40)
+          vni = raw >> 8;                                        // network_identifier (:45)
+          const GlobalReader ri{buf + off + po + 8u, len - off - po - 8u};
+          FlowWords g{};
+          const uint32_t s2 = decode<true>(ri, pl - 8u, g);
+          if (s2 == NPR_FLOW_OK) {
+            f = g;
+            st = NPR_FLOW_OK;
+          } else {
+            st = NPR_VXLAN_INNER + s2;
+          }
+        }
+      }
+    }
+  }
+  const bool ok = st == NPR_FLOW_OK;
+  const bool is6 = ok && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16));
+  uint4 r0, r1, s0, s1;
+  flow_rows(f, rc.offset, ok, is6, r0, r1, s0, s1);
+  if (status) status[i] = (uint8_t)st;
+  if (vni_out) vni_out[i] = vni;
+  if (flows) {
+    uint4 *dst = reinterpret_cast<uint4 *>(flows + i * 8);
+    dst[0] = r0;
+    dst[1] = r1;
+  }
+  if (flows_v6) {
+    uint4 *d6 = reinterpret_cast<uint4 *>(flows_v6 + i * 8);
+    d6[0] = s0;
+    d6[1] = s1;
+  }
+}
+
+hipError_t launch_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint32_t dst_port,
+                              bool big, uint32_t *flows, uint32_t *flows_v6, uint8_t *status, uint32_t *vni,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint64_t blocks = (n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(k_vxlan_flows, dim3((uint32_t)blocks), dim3(kBlock), 0, s, buf, len, recs, n, dst_port,
+                     big ? 1u : 0u, flows, flows_v6, status, vni);
   return hipGetLastError();
 }
 

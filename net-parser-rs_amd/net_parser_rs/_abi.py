@@ -35,6 +35,12 @@ KIND_UDP = 0x2
 OK, INCOMPLETE, FAILURE, CUSTOM = 0, 1, 2, 3
 OPT_PARK_FLOWS = 1  # npr_ctx_set_option: accepted for ABI 2 callers, no effect
 OPT_RESIDENT = 2    # npr_ctx_set_option: flows-only parses run the resident single pass (0 off, 1 auto, N>1 cap)
+# row f3 statuses (include/npr.h): outer failures keep their npr_flow_status code
+VXLAN_NOT_UDP = 32
+VXLAN_PORT = 33
+VXLAN_INCOMPLETE = 34
+VXLAN_INNER = 64  # + the inner frame's npr_flow_status
+VXLAN_PORT_IANA = 4789
 OPT_PIPE = 4  # npr_ctx_set_option: flows-only parses run the pipelined resident pass (1) or the contiguous one (0, default)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
@@ -98,7 +104,7 @@ EXPORTED = [
     "npr_parse_extract_pipelined", "npr_host_alloc", "npr_host_free",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
-    "npr_dev_convert_records",
+    "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -149,6 +155,10 @@ _SIGNATURES = {
                                              _vp, _vp, _vp, _vp]),
     "npr_dev_convert_records": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64,
                                                _vp, _vp, ctypes.c_uint64, _vp, _vp]),
+    "npr_dev_vxlan_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "npr_vxlan_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32,
+                                       ctypes.c_int, _vp, _vp, _vp, _vp]),
 }
 
 _lib = None

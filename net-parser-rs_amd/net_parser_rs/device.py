@@ -178,6 +178,21 @@ def dev_extract_flows(buf, recs, flows=None, flows_v6=None, status=None, ctx=Non
     return flows, flows_v6, status
 
 
+def dev_vxlan_flows(buf, recs, dst_port=0, big=True, ctx=None, stream=None):
+    """Row f3: the VXLAN inner flow of every device-resident record (npr_dev_vxlan_flows), async on
+    `stream`: dense (flows, flows_v6, status, vni) tensors, row i for record i."""
+    n = _dev_records(recs)
+    dev = buf.device
+    mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    flows, flows_v6, status, vni = mk(n * 32), mk(n * 32), mk(n), mk(n * 4)
+    ctx = ctx if ctx is not None else context(dev.index or 0)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    ctx.check(ctx.lib.npr_dev_vxlan_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n, int(dst_port),
+                                          _abi.BIG if big else _abi.LITTLE, flows.data_ptr(), flows_v6.data_ptr(),
+                                          status.data_ptr(), vni.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    return flows, flows_v6, status, vni
+
+
 def dev_convert_records(buf, recs, cap=None, out=None, out_v6=None, with_v6=True, ctx=None, stream=None):
     """flow::convert_records over device-resident records (npr_dev_convert_records), async on
     `stream`: (out, out_v6 or None, n_out) where rows [0, min(n_out, cap)) are the Ok flows in

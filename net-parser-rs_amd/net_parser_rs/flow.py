@@ -2,6 +2,8 @@
 import ctypes
 import ipaddress
 
+import struct
+
 import numpy as np
 
 from . import _abi
@@ -133,6 +135,62 @@ def convert_records(records):
         except FlowError:
             pass
     return out
+
+
+class Vxlan:
+    """layer4::Vxlan (src/layer4/vxlan.rs:7-49): the 8-byte VXLAN header and the rest as payload."""
+    __slots__ = ("flags", "group_policy_id", "raw_network_identifier", "network_identifier", "payload")
+
+    def __init__(self, flags, group_policy_id, raw_network_identifier, payload):
+        self.flags, self.group_policy_id = int(flags), int(group_policy_id)
+        self.raw_network_identifier = int(raw_network_identifier)
+        self.network_identifier = self.raw_network_identifier >> 8  # only 3 bytes are the VNI (:45)
+        self.payload = bytes(payload)
+
+    @staticmethod
+    def parse(data, endianness):
+        """Vxlan::parse (:31-48): (remainder, Vxlan); fewer than 8 bytes raise
+        net_parser_rs.Incomplete, like nom's u16!/u32! (the remainder is always empty: rest)."""
+        from . import Endianness, Incomplete
+        data = bytes(data)
+        if len(data) < 8:
+            raise Incomplete()
+        e = ">" if endianness == Endianness.Big else "<"
+        flags, gpid, raw = struct.unpack(e + "HHI", data[:8])
+        return b"", Vxlan(flags, gpid, raw, data[8:])
+
+    def as_bytes(self):
+        """Vxlan::as_bytes (:18-29): big-endian header + payload."""
+        return struct.pack(">HHI", self.flags, self.group_policy_id, self.raw_network_identifier) + self.payload
+
+
+def vxlan_flows(records, dst_port=0, big=True):
+    """Row f3: the VXLAN inner flow of each record (one device launch): a list of (record, Flow |
+    FlowError, vni).  A record whose outer frame is not an Ok UDP flow to dst_port (0: any) or whose
+    UDP payload is shorter than a VXLAN header gets a FlowError with the npr.h VXLAN code."""
+    from . import context
+    records = list(records)
+    if not records:
+        return []
+    bufs = {id(r._buf): r._buf for r in records}
+    if len(bufs) != 1:
+        out = []
+        for b in bufs.values():
+            out += vxlan_flows([r for r in records if r._buf is b], dst_port, big)
+        return out
+    ctx = context()
+    a = np.ascontiguousarray(next(iter(bufs.values())), dtype=np.uint8).reshape(-1)
+    t = _table(records)
+    n = len(t)
+    flows = np.zeros(n, dtype=_abi.FLOW_DTYPE)
+    v6 = np.zeros(n, dtype=_abi.FLOW_V6_DTYPE)
+    status = np.zeros(n, dtype=np.uint8)
+    vni = np.zeros(n, dtype=np.uint32)
+    ctx.check(ctx.lib.npr_vxlan_flows(ctx.handle, a.ctypes.data if a.size else None, a.size, t.ctypes.data, n,
+                                      int(dst_port), _abi.BIG if big else _abi.LITTLE, flows.ctypes.data,
+                                      v6.ctypes.data, status.ctypes.data, vni.ctypes.data))
+    return [(r, Flow._from_row(flows[i], v6[i]) if status[i] == 0 else FlowError(status[i]), int(vni[i]))
+            for i, r in enumerate(records)]
 
 
 class FlowExtraction:

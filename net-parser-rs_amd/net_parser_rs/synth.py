@@ -271,6 +271,73 @@ def quirk_corpus(n, seed=SEED + 7, big=False, with_header=True, jumbo_every=0, f
     return b"".join(parts)
 
 
+def _good_inner(rng):
+    """A valid inner frame: Ethernet (0-1 VLAN tags) / IPv4 (IHL 5) or IPv6 / TCP or UDP."""
+    macs = rng.integers(0, 256, size=12, dtype=np.uint8).tobytes()
+    tags = struct.pack(">HH", 0x8100, int(rng.integers(0, 65536))) if rng.integers(0, 4) == 0 else b""
+    proto = int(rng.choice([6, 17]))
+    pay = rng.integers(0, 256, size=int(rng.integers(0, 60)), dtype=np.uint8).tobytes()
+    ports = rng.integers(0, 256, size=4, dtype=np.uint8).tobytes()
+    if proto == 6:
+        l4 = bytearray(ports + rng.integers(0, 256, size=16, dtype=np.uint8).tobytes()) + pay
+        l4[12:14] = struct.pack(">H", (5 << 12) | int(rng.integers(0, 512)))
+    else:
+        l4 = bytearray(ports + struct.pack(">HH", 8 + len(pay), 0)) + pay
+    if rng.integers(0, 3):
+        ip = bytearray(rng.integers(0, 256, size=20, dtype=np.uint8).tobytes())
+        ip[0] = 0x45
+        ip[2:4] = struct.pack(">H", 20 + len(l4))
+        ip[9] = proto
+        return macs + tags + b"\x08\x00" + bytes(ip) + bytes(l4)
+    ip = bytearray(rng.integers(0, 256, size=40, dtype=np.uint8).tobytes())
+    ip[0] = 0x60 | (ip[0] & 0x0F)
+    ip[4:6] = struct.pack(">H", len(l4))
+    ip[6] = proto
+    return macs + tags + b"\x86\xdd" + bytes(ip) + bytes(l4)
+
+
+def _outer_udp(rng, payload, dport, v6=False):
+    """Ethernet / IPv4 (IHL 5) or IPv6 / UDP to `dport` carrying `payload` (all lengths exact)."""
+    macs = rng.integers(0, 256, size=12, dtype=np.uint8).tobytes()
+    udp = struct.pack(">HHHH", int(rng.integers(1024, 65536)), dport, 8 + len(payload), 0) + payload
+    if not v6:
+        ip = bytearray(rng.integers(0, 256, size=20, dtype=np.uint8).tobytes())
+        ip[0] = 0x45
+        ip[2:4] = struct.pack(">H", 20 + len(udp))
+        ip[9] = 17
+        return macs + b"\x08\x00" + bytes(ip) + udp
+    ip = bytearray(rng.integers(0, 256, size=40, dtype=np.uint8).tobytes())
+    ip[0] = 0x60
+    ip[4:6] = struct.pack(">H", len(udp))
+    ip[6] = 17
+    return macs + b"\x86\xdd" + bytes(ip) + udp
+
+
+def vxlan_corpus(n, seed=SEED + 11, with_header=True, port=4789):
+    """Row f3 corpus: VXLAN-encapsulated frames (valid inner flows, inner failures from the quirk
+    generator, truncated VXLAN headers, other UDP ports, IPv6 underlays) mixed with plain traffic."""
+    rng = np.random.default_rng(seed)
+    parts = [global_header()] if with_header else []
+    for i in range(n):
+        k = int(rng.integers(0, 10))
+        if k <= 3:    # VXLAN, valid inner frame
+            vx = struct.pack(">HHI", 0x0800, 0, int(rng.integers(0, 1 << 24)) << 8)
+            frame = _outer_udp(rng, vx + _good_inner(rng), port, v6=bool(rng.integers(0, 4) == 0))
+        elif k == 4:  # VXLAN, inner frame from the quirk generator (most fail somewhere)
+            vx = struct.pack(">HHI", int(rng.integers(0, 65536)), int(rng.integers(0, 65536)),
+                             int(rng.integers(0, 1 << 32)))
+            frame = _outer_udp(rng, vx + _frame(rng), port)
+        elif k == 5:  # UDP payload shorter than a VXLAN header
+            frame = _outer_udp(rng, rng.integers(0, 256, size=int(rng.integers(0, 8)), dtype=np.uint8).tobytes(), port)
+        elif k == 6:  # another UDP port
+            frame = _outer_udp(rng, rng.integers(0, 256, size=int(rng.integers(0, 40)), dtype=np.uint8).tobytes(),
+                               int(rng.choice([53, 5300, 4790])))
+        else:         # plain traffic (TCP, broken outer frames, ...)
+            frame = _frame(rng)
+        parts.append(struct.pack("<IIII", 1_600_000_000 + i, i % 1_000_000, len(frame), len(frame)) + frame)
+    return b"".join(parts)
+
+
 def corrupt_midfile(data, at_record, endianness_big=False):
     """Overwrite record `at_record`'s incl_len with a huge value (quirk Q3: the list stops there)."""
     buf = bytearray(data)

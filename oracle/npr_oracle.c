@@ -259,8 +259,9 @@ static void put_offset(npr_flow *f, uint64_t off) {
 }
 
 /* ---- src/flow/mod.rs:23-41 + src/flow/layer{2,3,4}/ (per-layer impls) ---------------------------------- */
-int or_extract_flow(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f,
-                    npr_flow_v6 *v6) {
+/* l4 / l4n (optional): the L4 header's start and length (the IP payload) of an Ok flow */
+static int extract_flow_l4(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f, npr_flow_v6 *v6,
+                           const uint8_t **l4_out, size_t *l4n_out) {
   or_eth e;
   int rc = or_eth_parse(p, n, &e); /* Ethernet::parse, mod.rs:28-31 */
   if (rc == OR_INCOMPLETE) return NPR_FLOW_ETH_INCOMPLETE;
@@ -330,7 +331,69 @@ int or_extract_flow(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow
   memcpy(f->dst_mac, e.dst_mac, 6);
   f->kind = (uint8_t)((v6flag ? NPR_FLOW_KIND_IPV6 : 0) | (udp ? NPR_FLOW_KIND_UDP : 0));
   put_offset(f, record_offset);
+  if (l4_out) *l4_out = l4;
+  if (l4n_out) *l4n_out = l4n;
   return NPR_FLOW_OK;
+}
+
+int or_extract_flow(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f, npr_flow_v6 *v6) {
+  return extract_flow_l4(p, n, record_offset, f, v6, NULL, NULL);
+}
+
+/* ---- row f3: src/layer4/vxlan.rs:31-48 (Vxlan::parse) + src/flow/layer4/vxlan.rs:32-50 ----- */
+int or_vxlan_parse(const uint8_t *in, size_t n, int big, or_vxlan *v) {
+  size_t pos = 0;
+  NEED(2); v->flags = rd_u16(in + pos, big); pos += 2;                   /* u16!(endianness) :38 */
+  NEED(2); v->group_policy_id = rd_u16(in + pos, big); pos += 2;         /* :39 */
+  NEED(4); v->raw_network_identifier = rd_u32(in + pos, big); pos += 4;  /* u32! :40 */
+  v->network_identifier = v->raw_network_identifier >> 8;                /* :45 */
+  v->payload_off = pos;                                                  /* rest :42 */
+  return OR_OK;
+}
+
+/* One record: the outer frame's flow must be Ok and UDP (to dst_port unless 0); its UDP payload
+ * is a VXLAN header + an inner Ethernet frame, whose flow is the result. */
+int or_vxlan_flow(const uint8_t *p, size_t n, uint64_t record_offset, uint32_t dst_port, int big, npr_flow *f,
+                  npr_flow_v6 *v6, uint32_t *vni) {
+  npr_flow outer;
+  const uint8_t *l4 = NULL;
+  size_t l4n = 0;
+  *vni = 0;
+  int st = extract_flow_l4(p, n, record_offset, &outer, NULL, &l4, &l4n);
+  if (st != NPR_FLOW_OK) return st;
+  if (!(outer.kind & NPR_FLOW_KIND_UDP)) return NPR_VXLAN_NOT_UDP;
+  if (dst_port && outer.dst_port != dst_port) return NPR_VXLAN_PORT;
+  or_l4 u;
+  if (or_udp_parse(l4, l4n, &u) != OR_OK) return NPR_VXLAN_INNER; /* (an Ok UDP flow re-parses) */
+  or_vxlan x;
+  if (or_vxlan_parse(l4 + u.payload_off, u.payload_len, big, &x) != OR_OK) return NPR_VXLAN_INCOMPLETE;
+  *vni = x.network_identifier;
+  /* Ethernet::parse(payload) then l2.extract_flow(); the remainder is always empty (:35-47) */
+  const uint8_t *inner = l4 + u.payload_off + x.payload_off;
+  st = or_extract_flow(inner, u.payload_len - x.payload_off, record_offset, f, v6);
+  return st == NPR_FLOW_OK ? NPR_FLOW_OK : NPR_VXLAN_INNER + st;
+}
+
+void or_vxlan_flows(const uint8_t *buf, size_t len, const npr_record *recs, size_t n, uint32_t dst_port, int big,
+                    npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status, uint32_t *vni) {
+  for (size_t i = 0; i < n; ++i) {
+    npr_flow f;
+    npr_flow_v6 v6;
+    uint32_t id = 0;
+    memset(&f, 0, sizeof f);
+    memset(&v6, 0, sizeof v6);
+    const size_t off = (size_t)recs[i].offset + 16, plen = recs[i].actual_length;
+    int st = (off > len || len - off < plen) ? -1
+                                             : or_vxlan_flow(buf + off, plen, recs[i].offset, dst_port, big, &f, &v6, &id);
+    if (st != NPR_FLOW_OK) {
+      memset(&f, 0, sizeof f);
+      memset(&v6, 0, sizeof v6);
+    }
+    if (flows) flows[i] = f;
+    if (flows_v6) flows_v6[i] = v6;
+    if (status) status[i] = (uint8_t)st;
+    if (vni) vni[i] = id;
+  }
 }
 
 static int record_flow(const uint8_t *buf, size_t len, const npr_record *r, npr_flow *f,

@@ -53,6 +53,18 @@ size_t or_convert_records(const uint8_t *buf, size_t len, const npr_record *recs
 void or_extract_flows(const uint8_t *buf, size_t len, const npr_record *recs, size_t n,
                       npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status);
 
+/* row f3: Vxlan::parse (src/layer4/vxlan.rs:31-48) and the VXLAN inner flow */
+typedef struct or_vxlan {
+  uint16_t flags, group_policy_id;
+  uint32_t raw_network_identifier, network_identifier;
+  size_t payload_off;
+} or_vxlan;
+int or_vxlan_parse(const uint8_t *in, size_t n, int big, or_vxlan *v);
+int or_vxlan_flow(const uint8_t *p, size_t n, uint64_t record_offset, uint32_t dst_port, int big, npr_flow *f,
+                  npr_flow_v6 *v6, uint32_t *vni);
+void or_vxlan_flows(const uint8_t *buf, size_t len, const npr_record *recs, size_t n, uint32_t dst_port, int big,
+                    npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status, uint32_t *vni);
+
 /* ---- layer-level parsers (pinned individually by the reference's layer KATs) ---- */
 typedef struct {
   const uint8_t *dst_mac, *src_mac;

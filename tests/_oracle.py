@@ -26,6 +26,12 @@ class OrEth(ctypes.Structure):
                 ("vlan", ctypes.c_uint16), ("n_vlans", ctypes.c_uint32), ("payload_off", _sz)]
 
 
+class OrVxlan(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint16), ("group_policy_id", ctypes.c_uint16),
+                ("raw_network_identifier", ctypes.c_uint32), ("network_identifier", ctypes.c_uint32),
+                ("payload_off", _sz)]
+
+
 class OrIp(ctypes.Structure):
     _fields_ = [("src", _vp), ("dst", _vp), ("protocol", ctypes.c_uint8),
                 ("payload_off", _sz), ("payload_len", _sz), ("rem", _sz)]
@@ -64,6 +70,10 @@ def lib():
         L.or_convert_records.restype = _sz
         L.or_extract_flows.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _vp]
         L.or_extract_flows.restype = None
+        L.or_vxlan_flows.argtypes = [_vp, _sz, _vp, _sz, ctypes.c_uint32, ctypes.c_int, _vp, _vp, _vp, _vp]
+        L.or_vxlan_flows.restype = None
+        L.or_vxlan_parse.argtypes = [_vp, _sz, ctypes.c_int, ctypes.POINTER(OrVxlan)]
+        L.or_vxlan_parse.restype = ctypes.c_int
         L.or_bench_extract.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _sz, _szp]
         L.or_bench_extract.restype = _sz
         L.or_bench_extract_mt.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _vp, _vp, _vp, _sz, _szp, ctypes.c_int]
@@ -140,6 +150,27 @@ def extract_flows(data, records):
     st = np.zeros(n, dtype=np.uint8)
     lib().or_extract_flows(p, a.size, recs.ctypes.data, n, flows.ctypes.data, v6.ctypes.data, st.ctypes.data)
     return flows, v6, st
+
+
+def vxlan_flows(data, records, dst_port=0, big=True):
+    """Row f3: the VXLAN inner flow of every record (dense): (flows, flows_v6, status, vni)."""
+    a, p = _buf(data)
+    n = len(records)
+    recs = np.ascontiguousarray(records, dtype=_abi.RECORD_DTYPE)
+    flows = np.zeros(n, dtype=_abi.FLOW_DTYPE)
+    v6 = np.zeros(n, dtype=_abi.FLOW_V6_DTYPE)
+    st = np.zeros(n, dtype=np.uint8)
+    vni = np.zeros(n, dtype=np.uint32)
+    lib().or_vxlan_flows(p, a.size, recs.ctypes.data, n, dst_port, 1 if big else 0, flows.ctypes.data,
+                         v6.ctypes.data, st.ctypes.data, vni.ctypes.data)
+    return flows, v6, st, vni
+
+
+def vxlan_parse(data, big=True):
+    """Vxlan::parse (src/layer4/vxlan.rs:31-48): (rc, OrVxlan)."""
+    a, p = _buf(data)
+    v = OrVxlan()
+    return lib().or_vxlan_parse(p, a.size, 1 if big else 0, ctypes.byref(v)), v
 
 
 def convert_records(data, records):

@@ -156,11 +156,19 @@ KATS = [
      "expect": {"src_port": 50871, "dst_port": 80, "layer4": "Udp"}},
     {"name": "encapsulated", "ref": "src/layer4/vxlan.rs:63-104", "api": "frame_layers",
      "input": VXLAN_ENCAP.hex(),
-     "expect": {"dst_mac": "08:00:27:f2:1d:8c", "dst_ip": "192.168.56.12", "udp_dst_port": 4789},
-     "derived": {"flow_status": 0, "src_ip": "192.168.56.11", "src_port": 48134, "layer4": "Udp"}},
+     "expect": {"dst_mac": "08:00:27:f2:1d:8c", "dst_ip": "192.168.56.12", "udp_dst_port": 4789,
+                # Vxlan::parse(udp.payload, Big) (:91-101): no remainder, flags, VNI, as_bytes
+                # round trip, then the inner Ethernet / IPv4 (:99-103)
+                "vxlan": {"ok": True, "remainder": 0, "flags": 0x0800, "network_identifier": 123,
+                          "as_bytes_is_udp_payload": True, "inner_dst_mac": "4a:7f:01:3b:a2:71",
+                          "inner_dst_ip": "10.0.0.2"}},
+     "derived": {"flow_status": 0, "src_ip": "192.168.56.11", "src_port": 48134, "layer4": "Udp",
+                 # the inner frame is ICMP: its Ethernet flow is Err(L3 IPv4 protocol)
+                 "vxlan_inner_flow_status": 15}},
     {"name": "not_encapsulated", "ref": "src/layer4/vxlan.rs:106-137", "api": "frame_layers",
      "input": VXLAN_PLAIN.hex(),
-     "expect": {"dst_mac": "00:86:9c:66:13:11", "dst_ip": "1.1.1.1", "udp_dst_port": 5300},
+     "expect": {"dst_mac": "00:86:9c:66:13:11", "dst_ip": "1.1.1.1", "udp_dst_port": 5300,
+                "vxlan": {"ok": False}},  # Vxlan::parse is Err on the 2-byte payload (:134-135)
      "derived": {"flow_status": 0, "src_ip": "192.168.0.216", "src_port": 60406, "layer4": "Udp"}},
     {"name": "format_flow", "ref": "src/flow/mod.rs:136-156", "api": "display_flow", "input": "",
      "flow": {"src_mac": "00:01:02:03:04:05", "src_ip": "0.1.2.3", "src_port": 80,
