@@ -137,12 +137,12 @@ typedef enum npr_flow_status {
  * quirk Q13): the outer frame's UDP payload parsed as Vxlan::parse (src/layer4/vxlan.rs:31-48),
  * then the inner Ethernet frame's flow as <Vxlan as FlowExtraction>::extract_flow
  * (src/flow/layer4/vxlan.rs:32-50).  Per-record status: an outer failure keeps its
- * npr_flow_status code (1..24); then: */
+  * flow status code, 1..24; then: */
 enum {
   NPR_VXLAN_NOT_UDP = 32,    /* the outer flow is Ok but TCP */
   NPR_VXLAN_PORT = 33,       /* the outer UDP destination port is not the one asked for */
   NPR_VXLAN_INCOMPLETE = 34, /* the UDP payload is shorter than the 8-B VXLAN header (Incomplete) */
-  NPR_VXLAN_INNER = 64       /* + the inner frame's npr_flow_status (1..24): the inner flow failed */
+  NPR_VXLAN_INNER = 64       /* + the inner frame's flow status code, 1..24: the inner flow failed */
 };
 
 /* Totals written by the device at the end of a parse.  `consumed` is where the record
