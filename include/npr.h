@@ -137,7 +137,7 @@ typedef enum npr_flow_status {
  * quirk Q13): the outer frame's UDP payload parsed as Vxlan::parse (src/layer4/vxlan.rs:31-48),
  * then the inner Ethernet frame's flow as <Vxlan as FlowExtraction>::extract_flow
  * (src/flow/layer4/vxlan.rs:32-50).  Per-record status: an outer failure keeps its
-  * flow status code, 1..24; then: */
+ * flow status code, 1..24; then: */
 enum {
   NPR_VXLAN_NOT_UDP = 32,    /* the outer flow is Ok but TCP */
   NPR_VXLAN_PORT = 33,       /* the outer UDP destination port is not the one asked for */
