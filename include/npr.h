@@ -371,6 +371,17 @@ npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
  * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
  * cap are not written), *n_out (a device word) = the number of Ok flows, or UINT64_MAX when the
  * launch's bounded look-back timed out.  One kernel pass. */
+/* The distinct-flow table (row f4; new, not in the reference): one row per distinct
+ * {family, protocol, src ip, dst ip, src port, dst port} of a device flow table (flows[0..n),
+ * flows_v6 its IPv6 side rows or NULL for an IPv4-only table), in the order of the input rows that
+ * first carry it.  out[k] = the flow of its first-seen record (lowest record offset, kept in the
+ * row), out_v6[k] its side row, counts[k] = the sum of weights[] over its rows (1 per row when
+ * weights is NULL; pass a previous call's counts to merge tables, e.g. one per GPU).  Rows past
+ * cap are not written; *n_out (a device word) = the number of distinct flows.  Asynchronous on
+ * `stream`; any of out_v6 / counts may be NULL. */
+npr_status npr_dev_flow_aggregate(npr_ctx *ctx, const npr_flow *flows, const npr_flow_v6 *flows_v6,
+                                  const uint64_t *weights, uint64_t n, npr_flow *out, npr_flow_v6 *out_v6,
+                                  uint64_t *counts, uint64_t cap, uint64_t *n_out, void *stream);
 /* VXLAN inner flows of device-resident records (row f3): dense outputs, row i for record i.
  * flows[i] = the INNER frame's flow with records[i]'s offset when status[i] == NPR_FLOW_OK
  * (zero row otherwise), flows_v6[i] its IPv6 addresses, vni[i] = the VXLAN network identifier

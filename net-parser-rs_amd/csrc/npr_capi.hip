@@ -46,7 +46,7 @@ struct npr_ctx {
   uint32_t sum_epoch[2] = {0, 0};
   uint32_t sum_next = 0;
   // staging for the host-memory entry points
-  DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6;
+  DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, agg;
   // host flows-only parses: the capture's H2D copy in chunks on copy_stream, each chunk's chained
   // launch as soon as its bytes (and the next chunk's, for records that straddle) have landed
   uint64_t stream_chunk = 0;  // NPR_OPT_STREAM_CHUNK (KiB in the option; 0 = one copy, the default)
@@ -209,7 +209,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->chain, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
-                    &c->flows2_v6})
+                    &c->flows2_v6, &c->agg})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
   if (c->summary) (void)hipFree(c->summary);
@@ -610,6 +610,19 @@ static npr_status convert_launch(npr_ctx *c, const void *input, uint64_t len, co
   HIP_CHECK(c, npr::launch_convert_records((const uint8_t *)input, len, recs, n, (uint32_t *)out, (uint32_t *)out_v6,
                                            cap, (uint64_t *)c->slots.p, c->epoch, total,
                                            kTimeoutTicks, s));
+  return NPR_OK;
+}
+
+npr_status npr_dev_flow_aggregate(npr_ctx *c, const npr_flow *flows, const npr_flow_v6 *flows_v6,
+                                  const uint64_t *weights, uint64_t n, npr_flow *out, npr_flow_v6 *out_v6,
+                                  uint64_t *counts, uint64_t cap, uint64_t *n_out, void *stream) {
+  if (!c || (!flows && n) || !n_out || (!out && cap)) return fail(c, NPR_ERR_ARG, "null argument");
+  if (n > 0xffffffffull) return fail(c, NPR_ERR_ARG, "at most 2^32 - 1 flow rows per call");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = ensure(c, c->agg, npr::flow_table_bytes(n));
+  if (st) return st;
+  HIP_CHECK(c, npr::launch_flow_aggregate((const uint32_t *)flows, (const uint32_t *)flows_v6, weights, n, c->agg.p,
+                                          (uint32_t *)out, (uint32_t *)out_v6, counts, cap, n_out, pick(c, stream)));
   return NPR_OK;
 }
 

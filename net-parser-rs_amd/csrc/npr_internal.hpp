@@ -140,6 +140,12 @@ hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_reco
 hipError_t launch_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint32_t dst_port,
                               bool big, uint32_t *flows, uint32_t *flows_v6, uint8_t *status, uint32_t *vni,
                               hipStream_t s);
+// row f4: the distinct-flow table (npr_flowtable.hip).  work: flow_table_bytes(n) bytes (any
+// content); out / out_v6 / counts: up to cap rows; *total = the number of distinct flows.
+hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6, const uint64_t *weights, uint64_t n,
+                                 void *work, uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap,
+                                 uint64_t *total, hipStream_t s);
+uint64_t flow_table_bytes(uint64_t n);
 // convert_records in one pass (k_convert_records): rows 0.. = Ok flows in reverse record order,
 // *total = all Ok flows (rows past cap are not written; ~0 when a bounded wait timed out).
 // look: convert_look_words(n) granules whose tags are not `epoch` at launch.

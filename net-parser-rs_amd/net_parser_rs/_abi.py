@@ -104,7 +104,7 @@ EXPORTED = [
     "npr_parse_extract_pipelined", "npr_host_alloc", "npr_host_free",
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
-    "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows",
+    "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -157,6 +157,8 @@ _SIGNATURES = {
                                                _vp, _vp, ctypes.c_uint64, _vp, _vp]),
     "npr_dev_vxlan_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint32,
                                            ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
+    "npr_dev_flow_aggregate": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_uint64, _vp, _vp, _vp, ctypes.c_uint64,
+                                              _vp, _vp]),
     "npr_vxlan_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32,
                                        ctypes.c_int, _vp, _vp, _vp, _vp]),
 }

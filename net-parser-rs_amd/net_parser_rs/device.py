@@ -178,6 +178,30 @@ def dev_extract_flows(buf, recs, flows=None, flows_v6=None, status=None, ctx=Non
     return flows, flows_v6, status
 
 
+def dev_flow_aggregate(flows, flows_v6=None, n=None, weights=None, cap=None, ctx=None, stream=None):
+    """Row f4: the distinct-flow table of a device flow table (npr_dev_flow_aggregate), async on
+    `stream`.  flows / flows_v6: CUDA uint8 tensors of 32-B rows (e.g. Workspace.flow_rows());
+    weights: CUDA int64 counts per row (merging aggregated tables) or None.  Returns (out, out_v6,
+    counts, n_out) with n_out a one-element CUDA int64 tensor: rows [0, min(n_out, cap)) valid."""
+    assert flows.is_cuda and flows.dtype == torch.uint8 and flows.is_contiguous()
+    n = flows.numel() // 32 if n is None else int(n)
+    dev = flows.device
+    cap = n if cap is None else int(cap)
+    mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
+    out, out_v6 = mk(cap * 32), mk(cap * 32)
+    counts = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+    n_out = torch.zeros(1, dtype=torch.int64, device=dev)
+    if weights is not None:
+        assert weights.is_cuda and weights.dtype == torch.int64 and weights.numel() >= n
+    ctx = ctx if ctx is not None else context(dev.index or 0)
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    p = lambda t: t.data_ptr() if t is not None else None
+    ctx.check(ctx.lib.npr_dev_flow_aggregate(ctx.handle, flows.data_ptr(), p(flows_v6), p(weights), n, out.data_ptr(),
+                                             out_v6.data_ptr(), counts.data_ptr(), cap, n_out.data_ptr(),
+                                             ctypes.c_void_p(s.cuda_stream)))
+    return out, out_v6, counts, n_out
+
+
 def dev_vxlan_flows(buf, recs, dst_port=0, big=True, ctx=None, stream=None):
     """Row f3: the VXLAN inner flow of every device-resident record (npr_dev_vxlan_flows), async on
     `stream`: dense (flows, flows_v6, status, vni) tensors, row i for record i."""

@@ -338,6 +338,49 @@ def vxlan_corpus(n, seed=SEED + 11, with_header=True, port=4789):
     return b"".join(parts)
 
 
+def flow_mix(n, n_flows=500, seed=SEED + 13, with_header=True):
+    """Row f4 corpus: n records drawn from a population of n_flows 5-tuples (IPv4 / IPv6, TCP / UDP,
+    Zipf-like popularity), with per-record MACs, VLAN tags and payloads that are not part of the
+    key, plus some frames that yield no flow."""
+    rng = np.random.default_rng(seed)
+    pop = []
+    for _ in range(n_flows):
+        v6 = bool(rng.integers(0, 4) == 0)
+        pop.append((v6, int(rng.choice([6, 17])), rng.integers(0, 256, size=32 if v6 else 8, dtype=np.uint8).tobytes(),
+                    int(rng.integers(0, 65536)), int(rng.integers(0, 65536))))
+    weights = 1.0 / np.arange(1, n_flows + 1)
+    picks = rng.choice(n_flows, size=n, p=weights / weights.sum())
+    parts = [global_header()] if with_header else []
+    for i in range(n):
+        if rng.integers(0, 20) == 0:
+            frame = _frame(rng)  # mostly no flow
+        else:
+            v6, proto, ips, sp, dp = pop[picks[i]]
+            pay = rng.integers(0, 256, size=int(rng.integers(0, 30)), dtype=np.uint8).tobytes()
+            if proto == 6:
+                l4 = bytearray(struct.pack(">HH", sp, dp) + rng.integers(0, 256, size=16, dtype=np.uint8).tobytes())
+                l4[12:14] = struct.pack(">H", 5 << 12)
+                l4 = bytes(l4) + pay
+            else:
+                l4 = struct.pack(">HHHH", sp, dp, 8 + len(pay), 0) + pay
+            macs = rng.integers(0, 256, size=12, dtype=np.uint8).tobytes()
+            tag = struct.pack(">HH", 0x8100, int(rng.integers(0, 65536))) if rng.integers(0, 5) == 0 else b""
+            if v6:
+                ip = bytearray(rng.integers(0, 256, size=8, dtype=np.uint8).tobytes())
+                ip[0] = 0x60
+                ip[4:6] = struct.pack(">H", len(l4))
+                ip[6] = proto
+                frame = macs + tag + b"\x86\xdd" + bytes(ip) + ips + l4
+            else:
+                ip = bytearray(rng.integers(0, 256, size=12, dtype=np.uint8).tobytes())
+                ip[0] = 0x45
+                ip[2:4] = struct.pack(">H", 20 + len(l4))
+                ip[9] = proto
+                frame = macs + tag + b"\x08\x00" + bytes(ip) + ips + l4
+        parts.append(struct.pack("<IIII", 1_600_000_000 + i, i % 1_000_000, len(frame), len(frame)) + frame)
+    return b"".join(parts)
+
+
 def corrupt_midfile(data, at_record, endianness_big=False):
     """Overwrite record `at_record`'s incl_len with a huge value (quirk Q3: the list stops there)."""
     buf = bytearray(data)

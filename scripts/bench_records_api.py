@@ -90,6 +90,17 @@ def main():
         passes += 1
     cpu_ms = (time.perf_counter() - t0) * 1e3 / passes
 
+    # row f4: the distinct-flow table over the convert_records table just made (C2: all distinct) and
+    # over a Zipf mix of 5000 5-tuples
+    agg_ms = timed_events(lambda: device.dev_flow_aggregate(out, out6, n=n, ctx=ctx, stream=stream), args.steps, stream)
+    mix = synth.flow_mix(n, n_flows=5000)
+    rcm, _, recm, _ = _oracle.capture_file_parse(mix)
+    fm, f6m = _oracle.convert_records(mix, recm)
+    fmt = torch.from_numpy(fm.view(np.uint8).copy()).to(dev)
+    f6t = torch.from_numpy(f6m.view(np.uint8).copy()).to(dev)
+    nm = len(fm)
+    agg_mix_ms = timed_events(lambda: device.dev_flow_aggregate(fmt, f6t, n=nm, ctx=ctx, stream=stream), args.steps,
+                              stream)
     cvt_bytes = n * (24 + 64) + len(want_f) * 64
     ext_bytes = n * (24 + 64 + 64 + 1)
     res = {
@@ -100,6 +111,9 @@ def main():
         "dev_extract_flows": {"kernel_ms": round(ext_ms, 5), "Mrecords_per_s": round(n / ext_ms / 1e3, 1),
                               "alg_bytes": ext_bytes, "GBps": round(ext_bytes / ext_ms / 1e6, 1),
                               "frac_of_8TBps": round(ext_bytes / ext_ms / 1e6 / 8000, 4)},
+        "dev_flow_aggregate": {"c2_all_distinct_ms": round(agg_ms, 5), "zipf_5000_flows_ms": round(agg_mix_ms, 5),
+                               "rows": n, "zipf_rows": nm,
+                               "Mrows_per_s": round(n / agg_ms / 1e3, 1)},
         "host_convert_records": {"ms": round(host_ms, 3), "Mrecords_per_s": round(n / host_ms / 1e3, 1),
                                  "note": "pageable host buffers: capture + records H2D, flow rows D2H"},
         "cpu_oracle_convert_records": {"ms": round(cpu_ms, 3), "Mrecords_per_s": round(n / cpu_ms / 1e3, 2),

@@ -1,0 +1,108 @@
+"""Row f4: the distinct-flow table on the device (npr_dev_flow_aggregate) against the CPU checker
+derived from the oracle's per-record flows (tests/_flowtable_ref.py).
+
+Inputs are the device's own convert_records tables (right-aligned flow rows of a flows-only parse),
+so the chain device parse -> device aggregate is what is checked, bit for bit: the first-seen rows,
+their order, the counts, and the distinct count.  Merging (the multi-GPU use: one table per GPU,
+then an aggregate of the aggregates weighted by their counts) must equal one aggregate of all rows.
+"""
+import numpy as np
+import pytest
+import torch
+
+import _flowtable_ref
+import _oracle
+from net_parser_rs import _abi, device, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def device_table(blob):
+    n = len(blob) // 16 + 1
+    ws = device.Workspace(n, n, records=False, status=False)
+    buf = torch.from_numpy(np.frombuffer(blob, np.uint8).copy()).cuda()
+    ws.launch(buf, start=24)
+    sm = ws.check()
+    fl, f6 = ws.flow_rows()
+    return fl.clone(), f6.clone(), int(sm.n_flows)
+
+
+def check(fl, f6, n, weights=None, cap=None):
+    flows = fl[: n * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+    v6 = f6[: n * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE) if f6 is not None else np.zeros(n, _abi.FLOW_V6_DTYPE)
+    w = None if weights is None else weights.cpu().numpy()
+    rows, counts = _flowtable_ref.aggregate(flows, v6, w)
+    out, out6, cnt, n_out = device.dev_flow_aggregate(fl, f6, n=n, weights=weights, cap=cap)
+    torch.cuda.synchronize()
+    k = int(n_out.item())
+    assert k == len(rows)
+    m = min(k, n if cap is None else cap)
+    assert out[: m * 32].cpu().numpy().tobytes() == flows[rows[:m]].tobytes()
+    if f6 is not None:
+        assert out6[: m * 32].cpu().numpy().tobytes() == v6[rows[:m]].tobytes()
+    assert np.array_equal(cnt[:m].cpu().numpy().astype(np.uint64), counts[:m])
+    return out, out6, cnt, k
+
+
+@pytest.mark.parametrize("n_flows", [1, 50, 5000])
+def test_flow_mix_matches_checker(n_flows):
+    blob = synth.flow_mix(40_000, n_flows=n_flows)
+    fl, f6, n = device_table(blob)
+    # the device table is the oracle's convert_records table
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    wf, _ = _oracle.convert_records(blob, recs)
+    assert fl.cpu().numpy().tobytes() == wf.tobytes()
+    check(fl, f6, n)
+
+
+def test_capacity_ipv4_only_and_empty():
+    blob = synth.flow_mix(10_000, n_flows=300, seed=3)
+    fl, f6, n = device_table(blob)
+    check(fl, f6, n, cap=17)
+    out, out6, cnt, n_out = device.dev_flow_aggregate(fl[:0], None, n=0)
+    torch.cuda.synchronize()
+    assert int(n_out.item()) == 0
+    c2 = synth.fixed64(20_000)  # IPv4 only, every 5-tuple distinct: no side table needed
+    fl2, _, n2 = device_table(c2)
+    _, _, cnt2, k2 = check(fl2, None, n2)
+    assert k2 == n2 and bool((cnt2[:k2] == 1).all())
+
+
+def test_merge_of_per_gpu_aggregates_equals_one_aggregate():
+    blob = synth.flow_mix(60_000, n_flows=2000, seed=9)
+    fl, f6, n = device_table(blob)
+    h = n // 2  # two "GPUs": rows [0, h) and [h, n) of the table
+    parts = [(fl[: h * 32], f6[: h * 32], h), (fl[h * 32: n * 32], f6[h * 32: n * 32], n - h)]
+    aggs = []
+    for a, a6, m in parts:
+        out, out6, cnt, n_out = device.dev_flow_aggregate(a.contiguous(), a6.contiguous(), n=m)
+        torch.cuda.synchronize()
+        k = int(n_out.item())
+        aggs.append((out[: k * 32], out6[: k * 32], cnt[:k], k))
+    cat = torch.cat([a[0] for a in aggs]).contiguous()
+    cat6 = torch.cat([a[1] for a in aggs]).contiguous()
+    w = torch.cat([a[2] for a in aggs]).contiguous()
+    mk = sum(a[3] for a in aggs)
+    check(cat, cat6, mk, weights=w)  # the merge itself, against the checker with weights
+    m_out, m_out6, m_cnt, m_n = device.dev_flow_aggregate(cat, cat6, n=mk, weights=w)
+    f_out, f_out6, f_cnt, f_n = device.dev_flow_aggregate(fl, f6, n=n)
+    torch.cuda.synchronize()
+    assert int(m_n.item()) == int(f_n.item())
+
+    def as_map(o, o6, c, k):
+        rows = o[: k * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+        r6 = o6[: k * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
+        ks = _flowtable_ref.keys(rows, r6)
+        return {key: (rows[i].tobytes(), int(c[i])) for i, key in enumerate(ks)}
+
+    assert as_map(m_out, m_out6, m_cnt, int(m_n.item())) == as_map(f_out, f_out6, f_cnt, int(f_n.item()))
+
+
+def test_c2_full_size_all_distinct():
+    blob = synth.fixed64(1_000_000)
+    fl, _, n = device_table(blob)
+    out, out6, cnt, n_out = device.dev_flow_aggregate(fl, None, n=n)
+    torch.cuda.synchronize()
+    assert int(n_out.item()) == n == 1_000_000
+    assert bool((cnt == 1).all())
+    assert torch.equal(out[: n * 32], fl[: n * 32])  # every row is its own first-seen row, input order kept
