@@ -75,37 +75,66 @@ __device__ __forceinline__ uint64_t row_offset(const uint32_t *row) {  // 40-bit
   return ((uint64_t)row[7] << 8) | (row[6] >> 24);
 }
 
+// One workgroup inserts kInsRows rows: each finds (or claims) its slot in the global table, then
+// the workgroup folds its rows per slot in an LDS table (count sum, first-seen minimum), so a
+// popular flow costs one pair of global atomics per workgroup, not one per row.
+constexpr int kInsPer = 4, kInsRows = kB * kInsPer, kLdsSlots = 2 * kInsRows;
+
 __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const uint32_t *flows_v6,
                                                    const uint64_t *weights, uint64_t n, uint64_t *slot_word,
                                                    uint64_t *slot_first, uint64_t *slot_count, uint32_t *slot_of_row,
                                                    uint64_t mask) {
-  const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t *row = flows + i * 8;
-  const Key k = row_key(row, flows_v6 ? flows_v6 + i * 8 : nullptr);
-  const uint64_t h = key_hash(k);
-  const uint32_t h32 = (uint32_t)(h >> 32) | 1u;  // never 0: 0 marks an empty slot
-  const uint64_t mine = ((uint64_t)h32 << 32) | (uint32_t)i;
-  uint64_t pos = h & mask;
-  for (;;) {
-    uint64_t w = __hip_atomic_load(slot_word + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (w == 0) {
-      uint64_t expect = 0;
-      if (__hip_atomic_compare_exchange_strong(slot_word + pos, &expect, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT))
-        break;  // claimed
-      w = expect;
-    }
-    if ((uint32_t)(w >> 32) == h32) {  // same hash: compare with the claiming row's key
-      const uint64_t j = (uint32_t)w;
-      const Key o = row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr);
-      if (key_eq(k, o)) break;
-    }
-    pos = (pos + 1) & mask;
+  __shared__ uint32_t lkey[kLdsSlots];
+  __shared__ unsigned long long lcnt[kLdsSlots], lfirst[kLdsSlots];
+  for (int e = threadIdx.x; e < kLdsSlots; e += kB) {
+    lkey[e] = ~0u;
+    lcnt[e] = 0;
+    lfirst[e] = ~0ull;
   }
-  atomicAdd((unsigned long long *)(slot_count + pos), (unsigned long long)(weights ? weights[i] : 1ull));
-  atomicMin((unsigned long long *)(slot_first + pos), (unsigned long long)row_offset(row));
-  slot_of_row[i] = (uint32_t)pos;
+  __syncthreads();
+  for (int q = 0; q < kInsPer; ++q) {
+    const uint64_t i = (uint64_t)blockIdx.x * kInsRows + (uint64_t)q * kB + threadIdx.x;
+    if (i >= n) continue;
+    const uint32_t *row = flows + i * 8;
+    const Key k = row_key(row, flows_v6 ? flows_v6 + i * 8 : nullptr);
+    const uint64_t h = key_hash(k);
+    const uint32_t h32 = (uint32_t)(h >> 32) | 1u;  // never 0: 0 marks an empty slot
+    const uint64_t mine = ((uint64_t)h32 << 32) | (uint32_t)i;
+    uint64_t pos = h & mask;
+    for (;;) {
+      uint64_t w = __hip_atomic_load(slot_word + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0) {
+        uint64_t expect = 0;
+        if (__hip_atomic_compare_exchange_strong(slot_word + pos, &expect, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;  // claimed
+        w = expect;
+      }
+      if ((uint32_t)(w >> 32) == h32) {  // same hash: compare with the claiming row's key
+        const uint64_t j = (uint32_t)w;
+        const Key o = row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr);
+        if (key_eq(k, o)) break;
+      }
+      pos = (pos + 1) & mask;
+    }
+    slot_of_row[i] = (uint32_t)pos;
+    // fold into the workgroup's LDS table (at most kInsRows distinct slots in 2x as many entries)
+    uint32_t e = (uint32_t)mix64(pos) & (kLdsSlots - 1);
+    for (;;) {
+      const uint32_t old = atomicCAS(&lkey[e], ~0u, (uint32_t)pos);
+      if (old == ~0u || old == (uint32_t)pos) break;
+      e = (e + 1) & (kLdsSlots - 1);
+    }
+    atomicAdd(&lcnt[e], (unsigned long long)(weights ? weights[i] : 1ull));
+    atomicMin(&lfirst[e], (unsigned long long)row_offset(row));
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kLdsSlots; e += kB) {
+    const uint32_t pos = lkey[e];
+    if (pos == ~0u) continue;
+    atomicAdd((unsigned long long *)(slot_count + pos), lcnt[e]);
+    atomicMin((unsigned long long *)(slot_first + pos), lfirst[e]);
+  }
 }
 
 // is row i its slot's first-seen row?  (record offsets are unique per row)
@@ -199,7 +228,7 @@ __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const
 
 }  // namespace
 
-uint64_t flow_table_slots(uint64_t n) {
+uint64_t flow_table_slots(uint64_t n) {  // (slot indices must fit the LDS table's u32 keys)
   uint64_t s = 1024;
   while (s < 2 * n) s <<= 1;
   return s;
@@ -221,7 +250,7 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
   if ((e = hipMemsetAsync(slot_word, 0, S * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(slot_first, 0xff, S * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(slot_count, 0, S * 8, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_agg_insert, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, flows_v6, weights, n,
+  hipLaunchKernelGGL(k_agg_insert, dim3((uint32_t)((n + kInsRows - 1) / kInsRows)), dim3(kB), 0, s, flows, flows_v6, weights, n,
                      slot_word, slot_first, slot_count, slot_of_row, S - 1);
   hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, flows, slot_of_row, slot_first, n, block);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(kB), 0, s, block, nb, total);
