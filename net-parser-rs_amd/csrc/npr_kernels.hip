@@ -1393,6 +1393,7 @@ __device__ __forceinline__ void res_wait(uint32_t ahead) {
 // (a window poll is 64 lanes x 5 granules): wait on ONE sentinel granule with a backed-off
 // s_sleep first, load whole windows only once it is there.
 __device__ __forceinline__ bool res_nap(const ParseParams &kp, uint64_t t0, uint32_t &nap) {
+  // (shorter naps, or the abort word read every 16th nap only, measured 3.5-4.5 us slower at C2)
   for (uint32_t i = 0; i < nap; ++i) __builtin_amdgcn_s_sleep(8);  // ~512 clocks each
   nap = nap < 2u ? nap * 2u : 2u;
   if (__hip_atomic_load(kp.abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kp.epoch) return false;
