@@ -1745,6 +1745,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   SpecCtx sc{};
   uint32_t wlast = kAnyLen;  // incl_len of the last record walked (walk_tile)
   uint64_t wait_ticks = 0;  // DIAG: phase A time spent waiting for tiles to land
+  uint64_t walk_ticks = 0;  // DIAG: ... walking the record chain
   for (uint32_t t = c0; t < c1; ++t) {
     const uint32_t k = t - c0, slot = k % kResRing;
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
@@ -1774,8 +1775,10 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       }
       if (pos != kNone && pos < tile_hi) {
         uint32_t n = 0;
+        const uint64_t tw1 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
         const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n, &wlast));
         wave_sync();
+        if (DIAG) walk_ticks += __builtin_amdgcn_s_memrealtime() - tw1;
         const uint32_t rounds = (n + 63u) >> 6;
         // a tile of few records (sparse captures) shares the last kept round when it fits there
         const bool pack = PACK && ns > 0 && fill + n <= 64u && n > 0;
@@ -2048,7 +2051,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     st.v[10] = c1 - tdef;
     st.v[11] = (entry != kNone && xe == pos) ? 1 : 0;
     st.v[15] = wait_ticks;
-    stamp_flush(kp, st, v, wid == 0 ? 0xFF7Fu : 0x8F7Fu);
+    st.v[7] = walk_ticks;
+    stamp_flush(kp, st, v, wid == 0 ? 0xFFFFu : 0x8FFFu);
   }
 }
 

@@ -1,7 +1,7 @@
 """Per-wave phase timings of k_parse_resident from bench.py --stats stamps (100 MHz ticks).
 [0] start [1] first tile landed [2] phase A done [3] A published + group fold [4] prefix known
 [5] kept flows written (fast path) [6] done; [8] tiles [9] kept rounds [10] deferred tiles [11] fast
-[15] ticks phase A spent waiting for its tiles to land"""
+[15] ticks phase A spent waiting for its tiles to land, [7] ticks walking the chain"""
 import sys
 
 import numpy as np
@@ -18,6 +18,7 @@ print("pctl            0     10     50     90     99    100")
 for k, nm in [(0, "start"), (1, "landed"), (2, "A done"), (3, "published"), (4, "prefix"), (6, "done")]:
     print(f"{nm:10s} {pc(S(k))}")
 print(f"{'A wait':10s} {pc(s[:, 15] / 100.0)}   (us waiting for tiles in phase A)")
+print(f"{'A walk':10s} {pc(s[:, 7] / 100.0)}   (us walking the chain in phase A)")
 for a, b, nm in [(0, 1, "first land"), (1, 2, "phase A"), (2, 3, "pub+fold"), (3, 4, "prefix wait"), (4, 6, "write")]:
     print(f"{nm:10s} {pc(S(b) - S(a))}")
 w0 = np.arange(0, nw, 16)
