@@ -32,10 +32,13 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "npr_internal.hpp"
 
 namespace npr {
 
+typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
 constexpr uint64_t kNone = ~0ull;
 constexpr uint64_t kMask48 = (1ull << 48) - 1;
 constexpr uint32_t kTsWindow = 1u << 20;  // speculation: |ts_sec delta| between neighbours
@@ -267,17 +270,46 @@ __device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f)
 // bit-identical to decode<> for these shapes.  Returns 0xff for any other frame (the caller then
 // runs the general decode<>).
 // ---------------------------------------------------------------------------------------------
-template <bool FIELDS>
+// A16: w is 16-byte aligned in LDS (the staged tiles; not the per-record rows)
+template <bool FIELDS, bool A16 = false>
 __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel, uint32_t n, FlowWords &f) {
   const uint32_t sh = rel & 3u;
-  const uint32_t *p = w + (rel >> 2);
   uint32_t a[17];
-  uint32_t prev = p[0];
+  // Every lane's window offset mod 16 the same (fixed-length records at a stride that is a
+  // multiple of 16, e.g. C2's 80 B): 16-B ds_read_b128 from the aligned base, conflict-free at
+  // such strides (the b32 reads at an 80-B stride are 4-way bank conflicts, MI355X_MICROARCH.md
+  // §LDS).  Otherwise per-dword reads.
+  const uint32_t m16 = rel & 15u, u16 = __builtin_amdgcn_readfirstlane(m16);
+  if (A16 && __ballot(m16 != u16) == 0ull) {
+    const u32x4 *q = reinterpret_cast<const u32x4 *>(w + ((rel & ~15u) >> 2));
+    auto fill = [&](auto J) {  // a[k] = bytes [rel + 4k, rel + 4k + 4): dwords J + k, J + k + 1
+      constexpr int j = decltype(J)::value;
+      uint32_t W[j + 18];
 #pragma unroll
-  for (int k = 0; k < 17; ++k) {
-    const uint32_t nx = p[k + 1];
-    a[k] = __builtin_amdgcn_alignbyte(nx, prev, sh);
-    prev = nx;
+      for (int c = 0; c < (j + 18 + 3) / 4; ++c) {
+        const u32x4 v = q[c];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (4 * c + e < j + 18) W[4 * c + e] = v[e];
+      }
+#pragma unroll
+      for (int k = 0; k < 17; ++k) a[k] = __builtin_amdgcn_alignbyte(W[j + k + 1], W[j + k], sh);
+    };
+    switch (u16 >> 2) {
+      case 0: fill(std::integral_constant<int, 0>{}); break;
+      case 1: fill(std::integral_constant<int, 1>{}); break;
+      case 2: fill(std::integral_constant<int, 2>{}); break;
+      default: fill(std::integral_constant<int, 3>{}); break;
+    }
+  } else {
+    const uint32_t *p = w + (rel >> 2);
+    uint32_t prev = p[0];
+#pragma unroll
+    for (int k = 0; k < 17; ++k) {
+      const uint32_t nx = p[k + 1];
+      a[k] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+      prev = nx;
+    }
   }
   // pin the window in registers: otherwise the backend turns the IPv4/IPv6 selects below into
   // divergent branches that each load only their own words (select-to-branch on loads)
@@ -338,7 +370,7 @@ template <bool FIELDS>
 __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo,
                                                uint32_t rel, FlowWords &f, bool valid = true) {
   const uint32_t incl = hdr(w, rel, 2, kp.big);
-  uint32_t st = decode_fast<FIELDS>(w, rel + 16u, incl, f);
+  uint32_t st = decode_fast<FIELDS, true>(w, rel + 16u, incl, f);
   if (__ballot(valid && st == 0xffu)) {  // uniform test: most tiles never take the general path
     if (valid && st == 0xffu) {
       const uint64_t p = tile_lo + rel;
@@ -906,7 +938,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-typedef unsigned int u32x4 __attribute__((__vector_size__(16)));
 // speculation context of this launch: ts_usec bound from the file magic, the first record's
 // ts_sec as a reference (both read once per wave)
 // Issue the (byte) loads of the speculation context: lanes 0..3 the pcap magic, lanes 4..7 the
