@@ -60,6 +60,12 @@ pub struct npr_flow {
     pub record_offset: [u8; 5],
 }
 
+// VXLAN statuses (include/npr.h): an outer failure keeps its flow status code
+pub const NPR_VXLAN_NOT_UDP: u8 = 32;
+pub const NPR_VXLAN_PORT: u8 = 33;
+pub const NPR_VXLAN_INCOMPLETE: u8 = 34;
+pub const NPR_VXLAN_INNER: u8 = 64;
+
 #[repr(C)]
 #[derive(Clone, Copy, Default, Debug)]
 pub struct npr_flow_v6 {
@@ -124,6 +130,22 @@ extern "C" {
         n_flows: *mut usize,
         consumed: *mut usize,
         chunk_bytes: u64,
+    ) -> npr_status;
+
+    /// Row f3: the VXLAN inner flow of each record (Vxlan::parse, src/layer4/vxlan.rs:31-48, then
+    /// <Vxlan as FlowExtraction>::extract_flow, src/flow/layer4/vxlan.rs:32-50); dense outputs
+    pub fn npr_vxlan_flows(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        records: *const npr_record,
+        n: usize,
+        dst_port: u32,
+        endianness: c_int,
+        flows: *mut npr_flow,
+        flows_v6: *mut npr_flow_v6,
+        status: *mut u8,
+        vni: *mut u32,
     ) -> npr_status;
 
     pub fn npr_host_alloc(ctx: *mut npr_ctx, bytes: usize, out: *mut *mut c_void) -> npr_status;

@@ -127,14 +127,111 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
     Ok((&input[consumed..], out))
 }
 
-// ---- device call ----------------------------------------------------------------------------
-/// One npr_extract_flows call over `payloads`: from `input` when every payload lies inside it
-/// behind its 16-byte record header, else from a staged buffer of [16 header bytes | payload]...
-fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow, Error>> {
+/// Row f3 (off the reference's flow path, which never yields a Vxlan flow): for each record, the
+/// outer frame's UDP payload (to `dst_port`, 0 = any; 4789 is the IANA port) parsed as
+/// `layer4::Vxlan::parse(.., endianness)` (src/layer4/vxlan.rs:31-48) and the inner Ethernet
+/// frame's flow, as `<Vxlan as FlowExtraction>::extract_flow` (src/flow/layer4/vxlan.rs:32-50),
+/// with the VXLAN network identifier (0 when the header was not reached).  One device call.
+/// Errors: an outer failure as extract_flow's; an inner Ethernet parse failure as
+/// `Error::L4(Vxlan(NetParser(..)))`; other inner failures as the inner frame's own flow error; a
+/// payload shorter than the VXLAN header as `Error::NetParser(Incomplete)`; an outer flow that is
+/// not UDP to `dst_port` as `Error::NetParser(Custom)`.
+pub fn vxlan_flows<'b>(
+    input: Option<&'b [u8]>,
+    records: &[PcapRecord<'b>],
+    dst_port: u16,
+    endianness: nom::Endianness,
+) -> Vec<(Result<Flow, Error>, u32)> {
+    let payloads: Vec<&[u8]> = records.iter().map(|r| r.payload).collect();
     let n = payloads.len();
     if n == 0 {
         return Vec::new();
     }
+    let (buf, recs) = stage(&payloads, input);
+    let mut flows = vec![ffi::npr_flow::default(); n];
+    let mut flows6 = vec![ffi::npr_flow_v6::default(); n];
+    let mut status = vec![0u8; n];
+    let mut vni = vec![0u32; n];
+    let r = with_ctx(|ctx| {
+        let st = unsafe {
+            ffi::npr_vxlan_flows(
+                ctx,
+                buf.as_ptr(),
+                buf.len(),
+                recs.as_ptr(),
+                n,
+                dst_port as u32,
+                crate::endian(endianness),
+                flows.as_mut_ptr(),
+                flows6.as_mut_ptr(),
+                status.as_mut_ptr(),
+                vni.as_mut_ptr(),
+            )
+        };
+        check(ctx, st)
+    });
+    if let Err(e) = r {
+        let msg = format!("{}", e);
+        return (0..n).map(|_| (Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() })), 0)).collect();
+    }
+    (0..n)
+        .map(|i| {
+            let st = status[i];
+            let res = match st {
+                0 => Ok(to_flow(&flows[i], &flows6[i])),
+                ffi::NPR_VXLAN_NOT_UDP | ffi::NPR_VXLAN_PORT => Err(Error::NetParser(crate::Error::Custom {
+                    msg: String::from("the outer flow is not UDP to the requested port"),
+                })),
+                ffi::NPR_VXLAN_INCOMPLETE => Err(Error::NetParser(crate::Error::Incomplete { size: None })),
+                s if s > ffi::NPR_VXLAN_INNER => {
+                    let inner = vxlan_inner(payloads[i]);
+                    match s - ffi::NPR_VXLAN_INNER {
+                        1 => Err(vxlan_eth_error(crate::Error::Incomplete { size: None })),
+                        2 => Err(vxlan_eth_error(crate::Error::Failure { msg: String::new() })),
+                        k => Err(flow_error(k, inner)),
+                    }
+                }
+                s => Err(flow_error(s, payloads[i])),
+            };
+            (res, vni[i])
+        })
+        .collect()
+}
+
+/// Error::L4(Vxlan(NetParser(e))) (src/flow/layer4/vxlan.rs:35-38)
+fn vxlan_eth_error(e: crate::Error) -> Error {
+    let v: layer4::vxlan::errors::Error = layer4::vxlan::errors::Error::NetParser(e);
+    let l4: layer4::errors::Error = v.into();
+    Error::L4(l4)
+}
+
+/// The inner Ethernet frame of an Ok outer Ethernet / IP / UDP frame carrying VXLAN: after the
+/// UDP header (8 B) and the VXLAN header (8 B); the L4 header starts 20 bytes into IPv4 (quirk Q7)
+/// and after one byte per extension in IPv6 (quirk Q11).
+fn vxlan_inner(p: &[u8]) -> &[u8] {
+    use crate::layer2::ethernet::{EthernetTypeId, Layer3Id};
+    let (et, l3) = l2_etype(p);
+    let l4 = match et {
+        EthernetTypeId::L3(Layer3Id::IPv6) => {
+            let get = |i: usize| p.get(l3 + i).copied().unwrap_or(0);
+            let mut k = 7;
+            let mut id = get(6);
+            while matches!(id, 0 | 43 | 44 | 50 | 51 | 60) {
+                id = get(k);
+                k += 1;
+            }
+            l3 + k + 33
+        }
+        _ => l3 + 20,
+    };
+    p.get(l4 + 16..).unwrap_or(&[])
+}
+
+// ---- device call ----------------------------------------------------------------------------
+/// The buffer and record rows one device call reads: `input` itself when every payload lies
+/// inside it behind its 16-byte record header, else a staged buffer of [16 header bytes | payload]...
+fn stage<'a>(payloads: &[&[u8]], input: Option<&'a [u8]>) -> (Cow<'a, [u8]>, Vec<ffi::npr_record>) {
+    let n = payloads.len();
     let inside = |buf: &[u8]| {
         let b = buf.as_ptr() as usize;
         payloads.iter().all(|p| {
@@ -142,7 +239,7 @@ fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow
             a >= b + 16 && a + p.len() <= b + buf.len()
         })
     };
-    let (buf, recs): (Cow<[u8]>, Vec<ffi::npr_record>) = match input {
+    match input {
         Some(buf) if inside(buf) => {
             let b = buf.as_ptr() as usize;
             let recs = payloads
@@ -170,7 +267,16 @@ fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow
             }
             (Cow::Owned(staged), recs)
         }
-    };
+    }
+}
+
+/// One npr_extract_flows call over `payloads` (read from `input` when they lie inside it).
+fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow, Error>> {
+    let n = payloads.len();
+    if n == 0 {
+        return Vec::new();
+    }
+    let (buf, recs) = stage(payloads, input);
     let mut flows = vec![ffi::npr_flow::default(); n];
     let mut flows6 = vec![ffi::npr_flow_v6::default(); n];
     let mut status = vec![0u8; n];

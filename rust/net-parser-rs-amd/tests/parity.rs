@@ -112,3 +112,70 @@ fn readme_facade() {
     let flow = packet.extract_flow().expect("Could not extract flow");
     assert_eq!(flow.destination.port, 80);
 }
+
+/// Eth/IPv4/UDP to 4789 carrying VXLAN + an inner Eth/IPv4/TCP frame, every 3rd record a
+/// VXLAN payload cut short of its 8-byte header, every 5th one sent to another port.
+fn vxlan_capture() -> Vec<u8> {
+    let mut v = vec![0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0];
+    v.extend_from_slice(&[0u8; 8]);
+    v.extend_from_slice(&65535u32.to_le_bytes());
+    v.extend_from_slice(&1u32.to_le_bytes());
+    for i in 0..600u32 {
+        let mut inner: Vec<u8> = (0..12).map(|k| (i as u8).wrapping_add(k)).collect();
+        inner.extend_from_slice(&[0x08, 0x00, 0x45, 0x00, 0, 40, 0, 0, 0, 0, 64, 6, 0, 0]);
+        inner.extend_from_slice(&[172, 16, (i >> 8) as u8, i as u8, 10, 1, 2, 3]);
+        inner.extend_from_slice(&((2000 + i) as u16).to_be_bytes());
+        inner.extend_from_slice(&443u16.to_be_bytes());
+        inner.extend_from_slice(&[0u8; 8]);
+        inner.extend_from_slice(&[0x50, 0x10, 0, 0, 0, 0, 0, 0]);
+        let mut vx = vec![0x08, 0x00, 0x00, 0x00];
+        vx.extend_from_slice(&((i * 977) << 8).to_be_bytes());
+        vx.extend_from_slice(&inner);
+        if i % 3 == 2 {
+            vx.truncate(5);
+        }
+        let port: u16 = if i % 5 == 4 { 4790 } else { 4789 };
+        let udp_len = 8 + vx.len() as u16;
+        let mut f: Vec<u8> = (0..12).map(|k| (i as u8).wrapping_mul(3).wrapping_add(k)).collect();
+        f.extend_from_slice(&[0x08, 0x00, 0x45, 0x00]);
+        f.extend_from_slice(&(20 + udp_len).to_be_bytes());
+        f.extend_from_slice(&[0, 0, 0, 0, 64, 17, 0, 0, 10, 0, 0, 1, 10, 0, 0, 2]);
+        f.extend_from_slice(&((40000 + i) as u16).to_be_bytes());
+        f.extend_from_slice(&port.to_be_bytes());
+        f.extend_from_slice(&udp_len.to_be_bytes());
+        f.extend_from_slice(&[0, 0]);
+        f.extend_from_slice(&vx);
+        v.extend_from_slice(&1_600_000_000u32.to_le_bytes());
+        v.extend_from_slice(&i.to_le_bytes());
+        v.extend_from_slice(&(f.len() as u32).to_le_bytes());
+        v.extend_from_slice(&(f.len() as u32).to_le_bytes());
+        v.extend_from_slice(&f);
+    }
+    v
+}
+
+#[test]
+fn vxlan_inner_flows_match_reference() {
+    use net_parser_rs::flow::layer2::FlowExtraction as _;
+    let data = vxlan_capture();
+    let (_, fa) = amd::parse(&data).unwrap();
+    let recs = fa.records.into_inner();
+    let got = amd::flow::vxlan_flows(Some(&data), &recs, 4789, nom::Endianness::Big);
+    assert_eq!(got.len(), 600);
+    for (i, (r, (res, vni))) in recs.iter().zip(got.iter()).enumerate() {
+        let udp_payload = &r.payload[14 + 20 + 8..];
+        if i % 5 == 4 {
+            assert!(res.is_err(), "record {}: other port", i);
+            continue;
+        }
+        match net_parser_rs::layer4::Vxlan::parse(udp_payload, nom::Endianness::Big) {
+            Err(_) => assert!(res.is_err(), "record {}: short VXLAN header", i),
+            Ok((_, vx)) => {
+                assert_eq!(*vni, vx.network_identifier, "record {}", i);
+                let (_, l2) = net_parser_rs::layer2::ethernet::Ethernet::parse(vx.payload).unwrap();
+                let want = l2.extract_flow().unwrap();
+                assert_eq!(res.as_ref().unwrap(), &want, "record {}", i);
+            }
+        }
+    }
+}

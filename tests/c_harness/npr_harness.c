@@ -111,6 +111,26 @@ static void run(npr_ctx *ctx, const char *path) {
             same_flows(fl, fl6, ofl, ofl6, nf),
         "%s: convert_records (%zu vs %zu)", path, nf, onf);
 
+  /* VXLAN inner flows (src/layer4/vxlan.rs:31-48 under the UDP step of src/flow/layer4.rs) */
+  {
+    uint8_t *vst = calloc(cap, 1), *ovst = calloc(cap, 1);
+    uint32_t *vni = calloc(cap, sizeof *vni), *ovni = calloc(cap, sizeof *ovni);
+    /* network order, as the reference's VXLAN tests parse it (src/layer4/vxlan.rs:91) */
+    or_vxlan_flows(in, len, orec, on, 4789, 1, dfl, dfl6, ovst, ovni);
+    CHECK(npr_vxlan_flows(ctx, in, len, orec, on, 4789, NPR_BIG, fl, fl6, vst, vni) == NPR_OK,
+          "%s: vxlan_flows: %s", path, npr_ctx_last_error(ctx));
+    size_t bad = 0, ok = 0;
+    for (size_t i = 0; i < on; ++i) {
+      if (vst[i] != ovst[i]) { ++bad; continue; }
+      if (vst[i] != NPR_FLOW_OK) continue;
+      ++ok;
+      if (vni[i] != ovni[i] || !same_flows(&fl[i], &fl6[i], &dfl[i], &dfl6[i], 1)) ++bad;
+    }
+    CHECK(bad == 0, "%s: %zu vxlan rows differ", path, bad);
+    if (ok) printf("%s: %zu VXLAN inner flows\n", path, ok);
+    free(vst), free(ovst), free(vni), free(ovni);
+  }
+
   /* the fused `extract` step: npr_parse_extract (left-aligned) */
   size_t nr3 = 0, nf3 = 0, c3 = 0;
   CHECK(npr_parse_extract(ctx, in, len, &h, NULL, 0, &nr3, fl, fl6, cap, &nf3, &c3) == NPR_OK && nf3 == onf &&

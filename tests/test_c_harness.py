@@ -37,6 +37,7 @@ def test_harness_on_device(tmp_path):
         "quirk_be.pcap": synth.quirk_corpus(3_000, seed=92, big=True),
         "adversarial.pcap": synth.quirk_corpus(2_000, seed=93, fake_every=3, zero_every=7, jumbo_every=150,
                                                tail="truncated_payload"),
+        "vxlan.pcap": synth.vxlan_corpus(4_000),
         "short.pcap": synth.global_header()[:20],
     }
     paths = []
