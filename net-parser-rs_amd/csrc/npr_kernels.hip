@@ -850,6 +850,37 @@ constexpr int kWalkUnroll = 4;
 // wave walking consecutive tiles keeps hopping through variable-length traffic; NULL: unknown
 // (the first record tries a stride)
 constexpr uint32_t kAnyLen = ~0u;  // walk_tile: no previous record length known
+// incl_len of the record header at LDS byte r (wave-uniform) in the capture's byte order
+template <bool BIG>
+__device__ __forceinline__ uint32_t incl_at(const uint32_t *w, uint32_t r) {
+  const uint32_t i = (r >> 2) + 2u;
+  const uint32_t v = __builtin_amdgcn_alignbyte(w[i + 1], w[i], r & 3u);
+  return __builtin_amdgcn_readfirstlane(BIG ? __builtin_bswap32(v) : v);
+}
+
+// A run of hops through variable-length records, from the record at r (length incl, already
+// checked): each record's offset goes to srec[n] (every lane stores the one address: a broadcast,
+// no exec-mask switch); the run stops at hop_span or at a record that is not a plain hop (same
+// length as the previous one, or longer than a tile).  hop_span is 0 unless every record starting
+// inside the tile with incl <= kTile ends inside the capture, so no Incomplete test is needed
+// here.  Returns the next position.
+template <bool BIG>
+__device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, uint32_t r, uint32_t incl,
+                                            uint32_t hop_span, uint32_t &n, uint32_t &last) {
+  for (;;) {
+    srec[n] = (uint16_t)r;
+    ++n;
+    r += incl + 16u;
+    last = incl;
+    if (r >= hop_span) break;
+    incl = incl_at<BIG>(w, r);
+    uint32_t d;  // incl, or kTile + 1 when it repeats the last length: one compare to leave on
+    asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %1" : "=s"(d) : "s"(incl), "s"(last), "s"((uint32_t)kTile + 1u) : "scc");
+    if (d > (uint32_t)kTile) break;
+  }
+  return r;
+}
+
 __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
                               uint64_t tile_hi, uint64_t entry, uint32_t &n_out, uint32_t *last_io = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -857,26 +888,34 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
   const uint32_t span = (uint32_t)(tile_hi - tile_lo);
   const uint64_t av = kp.len - tile_lo;
   const uint32_t avail = av > 0xffffffffull ? 0xffffffffu : (uint32_t)av;  // bytes from tile_lo
-  uint64_t p = uni64(entry);
-  uint32_t n = 0;
-  uint32_t last = last_io ? *last_io : kAnyLen;  // the previous record's incl_len
-  while (p < tile_hi) {
-    const uint32_t r = (uint32_t)(p - tile_lo);
-    // wave-uniform (one address): readfirstlane keeps the chain position scalar
-    const uint32_t incl = __builtin_amdgcn_readfirstlane(hdr(w, r, 2, big));
+  const uint32_t hop_span = avail - span >= (uint32_t)kTile + 16u ? span : 0u;
+  uint32_t r = (uint32_t)(uni64(entry) - tile_lo);  // relative chain position (entry < tile_hi)
+  uint32_t n = 0;                                   // record offsets stored in srec
+  uint32_t last = last_io ? *last_io : kAnyLen;     // the previous record's incl_len
+  uint64_t exit_far = kNone;  // a record longer than a tile: the chain leaves at this offset
+  while (r < span) {
+    const uint32_t incl = big ? incl_at<true>(w, r) : incl_at<false>(w, r);
     if (last == kAnyLen) last = incl;
-    if (kp.len - p < 16 || kp.len - p - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
+    const uint32_t e = incl + 16u;
+    if (e < 16u || e > avail - r) {  // (32-bit test; exact below when avail was clamped)
+      const uint64_t room = av - r;
+      if (room < 16 || room - 16 < incl) break;  // Err(Incomplete) -> stop (:37-45)
+    }
     // a record longer than a tile (no stride to speculate on), or one whose length differs from
     // the previous record's (variable-length traffic: a stride guess would confirm only itself):
-    // one hop, one header read
-    if (incl > (uint32_t)kTile || incl != last) {
-      if (lane == 0) srec[n] = (uint16_t)r;
-      n += 1;
-      p += 16ull + incl;
+    // hops, one header read each
+    if (incl > (uint32_t)kTile) {  // the chain leaves the tile with this record
+      srec[n] = (uint16_t)r;
+      ++n;
       last = incl;
+      exit_far = tile_lo + r + 16ull + incl;
+      break;
+    }
+    if (incl != last) {
+      r = big ? hop_run<true>(w, srec, r, incl, hop_span, n, last) : hop_run<false>(w, srec, r, incl, hop_span, n, last);
       continue;
     }
-    const uint32_t stride = 16u + incl;
+    const uint32_t stride = e;
     if (span - r <= 64u * stride) {  // one header per lane reaches the tile's end: a single read
       const uint32_t q0 = r + lane * stride;
       uint32_t h0 = hdr(w, q0 < span ? q0 : 0u, 2, big);
@@ -885,7 +924,7 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
       const uint32_t m = (~b0 == 0ull) ? 64u : (uint32_t)__builtin_ctzll(~b0);
       srec[n + lane] = (uint16_t)q0;
       n += m;
-      p += (uint64_t)m * stride;
+      r += m * stride;
       continue;
     }
     uint64_t b[kWalkUnroll];
@@ -912,12 +951,11 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
 #pragma unroll
     for (int u = 0; u < kWalkUnroll; ++u) srec[n + lane + 64u * (uint32_t)u] = (uint16_t)qr[u];
     n += m;
-    p += (uint64_t)m * stride;
-    last = incl;
+    r += m * stride;
   }
   n_out = n;
   if (last_io) *last_io = last;
-  return p;
+  return exit_far != kNone ? exit_far : tile_lo + r;
 }
 
 // diagnostics (DIAG kernel variants only: the production kernels carry none of this)
