@@ -271,8 +271,10 @@ __device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f)
 // runs the general decode<>).
 // ---------------------------------------------------------------------------------------------
 // A16: w is 16-byte aligned in LDS (the staged tiles; not the per-record rows)
+// valid: lanes whose result is used (A16: when every such lane is IPv4, the IPv4-only variant)
 template <bool FIELDS, bool A16 = false>
-__device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel, uint32_t n, FlowWords &f) {
+__device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel, uint32_t n, FlowWords &f,
+                                                bool valid = true) {
   const uint32_t sh = rel & 3u;
   uint32_t a[17];
   // Every lane's window offset mod 16 the same (fixed-length records at a stride that is a
@@ -282,8 +284,10 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
   const uint32_t m16 = rel & 15u, u16 = __builtin_amdgcn_readfirstlane(m16);
   if (A16 && __ballot(m16 != u16) == 0ull) {
     const u32x4 *q = reinterpret_cast<const u32x4 *>(w + ((rel & ~15u) >> 2));
-    auto fill = [&](auto J) {  // a[k] = bytes [rel + 4k, rel + 4k + 4): dwords J + k, J + k + 1
+    // a[k] = bytes [rel + 4k, rel + 4k + 4): dwords J + k, J + k + 1 (Z: 4-aligned, dword J + k)
+    auto fill = [&](auto J, auto Z) {
       constexpr int j = decltype(J)::value;
+      constexpr bool z = decltype(Z)::value;
       uint32_t W[j + 18];
 #pragma unroll
       for (int c = 0; c < (j + 18 + 3) / 4; ++c) {
@@ -293,13 +297,22 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
           if (4 * c + e < j + 18) W[4 * c + e] = v[e];
       }
 #pragma unroll
-      for (int k = 0; k < 17; ++k) a[k] = __builtin_amdgcn_alignbyte(W[j + k + 1], W[j + k], sh);
+      for (int k = 0; k < 17; ++k) a[k] = z ? W[j + k] : __builtin_amdgcn_alignbyte(W[j + k + 1], W[j + k], sh);
     };
-    switch (u16 >> 2) {
-      case 0: fill(std::integral_constant<int, 0>{}); break;
-      case 1: fill(std::integral_constant<int, 1>{}); break;
-      case 2: fill(std::integral_constant<int, 2>{}); break;
-      default: fill(std::integral_constant<int, 3>{}); break;
+    using Y = std::true_type;
+    using N = std::false_type;
+    switch (u16) {  // (wave-uniform)
+      case 0: fill(std::integral_constant<int, 0>{}, Y{}); break;
+      case 4: fill(std::integral_constant<int, 1>{}, Y{}); break;
+      case 8: fill(std::integral_constant<int, 2>{}, Y{}); break;
+      case 12: fill(std::integral_constant<int, 3>{}, Y{}); break;
+      default:
+        switch (u16 >> 2) {
+          case 0: fill(std::integral_constant<int, 0>{}, N{}); break;
+          case 1: fill(std::integral_constant<int, 1>{}, N{}); break;
+          case 2: fill(std::integral_constant<int, 2>{}, N{}); break;
+          default: fill(std::integral_constant<int, 3>{}, N{}); break;
+        }
     }
   } else {
     const uint32_t *p = w + (rel >> 2);
@@ -325,8 +338,12 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
   // branches: divergent if/else here costs more scalar exec-mask work than the arithmetic).
   const uint32_t etype = be16(12), b0 = byte(14);
   const uint32_t proto4 = byte(23), nh = byte(20);
-  const bool v4 = (etype == 0x0800u) & (b0 == 0x45u) & (n >= 34u) & ((proto4 == 6u) | (proto4 == 17u));
-  const bool v6 = (etype == 0x86ddu) & ((b0 >> 4) == 6u) & (n >= 54u) & ((nh == 6u) | (nh == 17u));
+  const bool is4 = (etype == 0x0800u) & (b0 == 0x45u) & (n >= 34u) & ((proto4 == 6u) | (proto4 == 17u));
+  auto core = [&](auto ONLY4) -> uint32_t {
+  // ONLY4: every used lane is IPv4 (the selects below fold; unused lanes return garbage)
+  constexpr bool only4 = decltype(ONLY4)::value;
+  const bool v4 = only4 ? true : is4;
+  const bool v6 = only4 ? false : (etype == 0x86ddu) & ((b0 >> 4) == 6u) & (n >= 54u) & ((nh == 6u) | (nh == 17u));
   const uint32_t n3 = n - 14u;
   // IPv4 (IHL 5): wrapping u16 payload length; options/padding absent -> never a remainder
   const uint32_t length = v4 ? ((be16(16) - 20u) & 0xffffu) : be16(18);
@@ -363,6 +380,9 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
     f.v6off = 22u;
   }
   return (v4 | v6) ? (st3 ? st3 : st4) : 0xffu;
+  };
+  if (A16 && __ballot(valid & !is4) == 0ull) return core(std::true_type{});
+  return core(std::false_type{});
 }
 
 // one record (header at LDS offset rel) -> status (+ flow words); fast shape first
@@ -370,7 +390,7 @@ template <bool FIELDS>
 __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo,
                                                uint32_t rel, FlowWords &f, bool valid = true) {
   const uint32_t incl = hdr(w, rel, 2, kp.big);
-  uint32_t st = decode_fast<FIELDS, true>(w, rel + 16u, incl, f);
+  uint32_t st = decode_fast<FIELDS, true>(w, rel + 16u, incl, f, valid);
   if (__ballot(valid && st == 0xffu)) {  // uniform test: most tiles never take the general path
     if (valid && st == 0xffu) {
       const uint64_t p = tile_lo + rel;
@@ -1918,7 +1938,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       if (k == 0) __builtin_amdgcn_s_setprio(2);
       else if (k == 1) __builtin_amdgcn_s_setprio(1);
       else if (k == 2) __builtin_amdgcn_s_setprio(0);
-    } else {
+    } else if ((k & 3u) == 3u) {  // (every 4th tile: the update costs issue slots)
       if (lane == 0) sh.prog[wid] = k + 1;
       uint32_t mn = lane < kResWg ? sh.prog[lane] : ~0u;
 #pragma unroll
