@@ -411,7 +411,7 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
         ++n;
       }
       if (n >= 64) {  // 3/4 of the kept capacity at that many bytes per record
-        const uint64_t fit = (uint64_t)c->res_waves * npr::kResSlots * 64 * 3 / 4 * (off / n);
+        const uint64_t fit = (uint64_t)c->res_waves * npr::kResSlots * 64 * 7 / 8 * (off / n);
         chunk = std::max(dense, fit);
       }
       pack = chunk > dense;  // links past one kept round per tile: sparse tiles must share rounds
