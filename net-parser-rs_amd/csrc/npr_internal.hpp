@@ -53,12 +53,18 @@ struct alignas(128) RangeSlot {
   uint64_t pad[4];
 };
 static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
-constexpr uint32_t kResMaxWaves = 64 * 64;  // at most 4096 persistent waves
+#ifndef NPR_RES_MAX_WAVES
+#define NPR_RES_MAX_WAVES 4096
+#endif
+constexpr uint32_t kResMaxWaves = NPR_RES_MAX_WAVES;  // at most 4096 persistent waves
 #ifndef NPR_RES_SLOTS
 #define NPR_RES_SLOTS 6
 #endif
 constexpr int kResSlots = NPR_RES_SLOTS;    // 64-record rounds of flows held in registers per wave
-constexpr uint32_t kResWgMin = 16;          // waves per workgroup (npr_kernels.hip kResWg) is at least this
+#ifndef NPR_RES_WG_MIN
+#define NPR_RES_WG_MIN 16
+#endif
+constexpr uint32_t kResWgMin = NPR_RES_WG_MIN;  // waves per workgroup (npr_kernels.hip kResWg) is at least this
 
 // exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
 enum : int { kPreExit = 0, kPreCnt = 1, kPreOk = 2, kPreMism = 3, kPreEntry = 4 };

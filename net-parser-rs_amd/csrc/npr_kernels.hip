@@ -2145,14 +2145,20 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   }
 }
 
+#ifndef NPR_NO_PIPE  // (experiment builds whose tile geometry the pipelined pass does not fit)
 #include "npr_kernels_pipe.inc"
+#endif
 
 int pipe_waves_per_cu() {
+#ifdef NPR_NO_PIPE
+  return 0;
+#else
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_pipe<false>), kPipeWg * kWave, 0) !=
       hipSuccess)
     return 0;
   return nb * (int)kPipePar;  // parser waves
+#endif
 }
 
 int resident_waves_per_cu() {
@@ -2173,12 +2179,14 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
 }
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
+#ifndef NPR_NO_PIPE
   if (p.nwaves && p.pipe) {
     const uint32_t nb = p.nwaves / kPipePar;
     if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_pipe<true>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
     else hipLaunchKernelGGL((k_parse_pipe<false>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
     return hipGetLastError();
   }
+#endif
   if (p.nwaves) {
     const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
     const bool diag = p.stats || p.stamps;
