@@ -389,8 +389,14 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
 template <bool FIELDS>
 __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint32_t *w, uint64_t tile_lo,
                                                uint32_t rel, FlowWords &f, bool valid = true) {
-  const uint32_t incl = hdr(w, rel, 2, kp.big);
-  uint32_t st = decode_fast<FIELDS, true>(w, rel + 16u, incl, f, valid);
+  // lanes whose result is unused read what the first used lane reads: LDS broadcasts identical
+  // addresses, so they add no bank conflicts (a sparse tile has ~5 used lanes of 64; their stale
+  // offsets were random addresses: C3 46 % of LDS-active cycles conflicted)
+  const uint64_t vb = __ballot(valid);
+  const uint32_t rel0 = vb ? (uint32_t)__builtin_amdgcn_readlane((int)rel, (int)__builtin_ctzll(vb)) : 0u;
+  const uint32_t rr = valid ? rel : rel0;
+  const uint32_t incl = hdr(w, rr, 2, kp.big);
+  uint32_t st = decode_fast<FIELDS, true>(w, rr + 16u, incl, f, valid);
   if (__ballot(valid && st == 0xffu)) {  // uniform test: most tiles never take the general path
     if (valid && st == 0xffu) {
       const uint64_t p = tile_lo + rel;
