@@ -83,17 +83,20 @@ def cpu_baseline(blob, n_records, budget_s, sample):
                       f"parallel extract_flow); {p1} passes in {e1:.1f} s on 1 core"}
 
 
-def pmc_traffic(records):
-    """HBM-side bytes per launch from the newest committed PMC summary of this workload (profiles/),
-    or None.  Collected by scripts/pmc.sh: FETCH_SIZE x2 + WRITE_SIZE."""
+def pmc_traffic(records, config="c2"):
+    """HBM-side bytes per launch (C2) or per capture (C3: all its chained links) from the newest
+    committed PMC summary of this workload (profiles/), or None.  Collected by scripts/pmc.sh:
+    FETCH_SIZE x2 + WRITE_SIZE."""
     import glob
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if records == 1_000_000 and d.get("workload", "").startswith("C2"):
+        if config == "c2" and records == 1_000_000 and d.get("workload", "").startswith("C2"):
             return d.get("traffic_bytes_per_launch"), os.path.basename(f)
+        if config == "c3" and records == 8_000_000 and d.get("workload", "").startswith("C3"):
+            return d.get("traffic_bytes_per_capture"), os.path.basename(f)  # all chained links of one capture
     return None, None
 
 
@@ -160,7 +163,7 @@ def run_single(args, dev, local):
         stats_dump(ws, bufs, hdr, copies, 0)
     read_b = len(blob)   # every byte of the capture is read (C2: = SURVEY 8d's 16 + min(incl, 64) per record)
     write_b = 32 * n_flows
-    traffic, src = pmc_traffic(n) if args.config == "c2" else (None, None)
+    traffic, src = pmc_traffic(n, args.config) if args.config in ("c2", "c3") else (None, None)
     out = base_line(args, 1, wall, n, len(blob))
     out["config"].update({"records_per_gpu": n, "capture_bytes": len(blob), "parallelism": "single GPU"})
     out["roofline"] = roofline(read_b, write_b, kern_ms, traffic, src, stream_b=len(blob) - 24)

@@ -901,7 +901,10 @@ __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, u
     if (r >= hop_span) break;
     incl = incl_at<BIG>(w, r);
     uint32_t d;  // incl, or kTile + 1 when it repeats the last length: one compare to leave on
-    asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %1" : "=s"(d) : "s"(incl), "s"(last), "s"((uint32_t)kTile + 1u) : "scc");
+    asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %1"
+        : "=s"(d)
+        : "s"(incl), "s"(__builtin_amdgcn_readfirstlane(last)), "s"((uint32_t)kTile + 1u)
+        : "scc");  // (readfirstlane: an "s" operand the allocator had put in a VGPR fails to assemble)
     if (d > (uint32_t)kTile) break;
   }
   return r;
