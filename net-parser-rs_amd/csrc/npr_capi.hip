@@ -389,9 +389,11 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
   npr_status st = res_geometry(c);
   if (st) return st;
   uint64_t chunk = chunk_bytes;
-  bool pack = chunk_bytes > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
+  // the waves one link runs (NPR_OPT_RESIDENT N > 1 caps them, as launch_range does)
+  const uint64_t waves = c->resident > 1 ? std::min<uint64_t>(c->res_waves, (uint64_t)c->resident) : c->res_waves;
+  bool pack = chunk_bytes > waves * npr::kResSlots * npr::kTile;
   if (!chunk) {  // one launch keeps kResSlots rounds of 64 records per wave in registers
-    const uint64_t dense = (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;  // >= 64 records per tile
+    const uint64_t dense = waves * npr::kResSlots * npr::kTile;  // >= 64 records per tile
     chunk = dense;
     if (stop - start >= 8 * dense && !speculative_start && !sh) {
       // large: size the links by the record density of the capture's first 256 KiB, walked here from
@@ -411,7 +413,7 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
         ++n;
       }
       if (n >= 64) {  // 3/4 of the kept capacity at that many bytes per record
-        const uint64_t fit = (uint64_t)c->res_waves * npr::kResSlots * 64 * 7 / 8 * (off / n);
+        const uint64_t fit = waves * npr::kResSlots * 64 * 7 / 8 * (off / n);
         chunk = std::max(dense, fit);
       }
       pack = chunk > dense;  // links past one kept round per tile: sparse tiles must share rounds

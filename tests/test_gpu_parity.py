@@ -329,6 +329,26 @@ def test_chunked_chain_end_and_tails(chunk):
         check_chunked(synth.quirk_corpus(2_000, seed=56, tail=tail), chunk)
 
 
+@pytest.mark.parametrize("chunk", [333_333, 0])
+@pytest.mark.parametrize("corpus", ["c3", "quirk", "adversarial", "jumbo", "v6"])
+def test_chunked_packing_pass(corpus, chunk):
+    """At most 7 waves: links longer than one kept round per tile run the PACK instantiation
+    (sparse tiles share kept rounds, unused lanes read the first used lane's record, the IPv4-only
+    decode variant when it applies, deferred tiles once the kept rounds are full); chunk 0 = the
+    density-sized links (the capture is >= 8 x one dense link)."""
+    blob = {"c3": lambda: synth.variable_mix(8_000),
+            "quirk": lambda: synth.quirk_corpus(40_000, seed=58),
+            "adversarial": lambda: synth.quirk_corpus(20_000, seed=59, fake_every=3, zero_every=7, jumbo_every=150),
+            "jumbo": lambda: synth.quirk_corpus(1_500, seed=60, jumbo_every=2),
+            "v6": lambda: synth.quirk_corpus(30_000, seed=61, big=True)}[corpus]()
+    ctx = npr.context(0)
+    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 7))
+    try:
+        check_chunked(blob, chunk)
+    finally:
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+
+
 def test_chunked_bare_records_and_tiny_inputs():
     body = synth.quirk_corpus(3_000, seed=57, with_header=False)
     check_chunked(body, 5_000, start=0, endianness=npr.Endianness.Little)
