@@ -260,7 +260,8 @@ npr_status npr_extract_flows(npr_ctx *ctx, const uint8_t *input, size_t len,
                              const npr_record *records, size_t n, npr_flow *flows,
                              npr_flow_v6 *flows_v6, uint8_t *status);
 /* flow::convert_records (src/flow/mod.rs:101-123): Ok flows in reverse record order.
- * *n_out = number of flows (> cap => NPR_ERR_CAPACITY, nothing beyond cap written). */
+ * *n_out = number of flows (> cap => NPR_ERR_CAPACITY, nothing beyond cap written).
+ * out_v6[i] (optional) is written only when out[i] is IPv6. */
 npr_status npr_convert_records(npr_ctx *ctx, const uint8_t *input, size_t len,
                                const npr_record *records, size_t n, npr_flow *out,
                                npr_flow_v6 *out_v6, size_t cap, size_t *n_out);
@@ -369,8 +370,9 @@ npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
                                  npr_flow_v6 *flows_v6, uint8_t *status, void *stream);
 /* flow::convert_records (src/flow/mod.rs:101-123) over device-resident records, asynchronous on
  * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
- * cap are not written), *n_out (a device word) = the number of Ok flows, or UINT64_MAX when the
- * launch's bounded look-back timed out.  One kernel pass. */
+ * cap are not written; out_v6[i] only when out[i] is IPv6), *n_out (a device word) = the number of
+ * Ok flows, or UINT64_MAX when the launch's bounded look-back timed out.  One kernel pass
+ * (DESIGN.md §3.4). */
 /* The distinct-flow table (row f4; new, not in the reference): one row per distinct
  * {family, protocol, src ip, dst ip, src port, dst port} of a device flow table (flows[0..n),
  * flows_v6 its IPv6 side rows or NULL for an IPv4-only table), in the order of the input rows that

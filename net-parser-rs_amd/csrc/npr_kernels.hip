@@ -2587,14 +2587,12 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
         uint4 *dst = reinterpret_cast<uint4 *>(out + rw * 8);
         dst[0] = make_uint4(is6 ? 0u : kd[r][0], kd[r][1], kd[r][2], kd[r][3]);
         dst[1] = make_uint4(kd[r][4], kd[r][5], kd[r][6] | ((uint32_t)(koff[r] & 0xffu) << 24), (uint32_t)(koff[r] >> 8));
-        if (out_v6) {
-          uint32_t a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (is6) {  // the 32 address bytes, re-read (rare; the payload lies inside the buffer)
-            const uint64_t po = koff[r] + 16;
-            GlobalReader g{buf + po, len - po};
+        if (out_v6 && is6) {  // side rows of IPv6 flows only (as the resident pass: npr.h)
+          uint32_t a[8];
+          const uint64_t po = koff[r] + 16;  // the 32 address bytes, re-read (the payload lies inside the buffer)
+          GlobalReader g{buf + po, len - po};
 #pragma unroll
-            for (int k = 0; k < 8; ++k) a[k] = g.le32(kd[r][0] + 4u * k);
-          }
+          for (int k = 0; k < 8; ++k) a[k] = g.le32(kd[r][0] + 4u * k);
           uint4 *d6 = reinterpret_cast<uint4 *>(out_v6 + rw * 8);
           d6[0] = make_uint4(a[0], a[1], a[2], a[3]);
           d6[1] = make_uint4(a[4], a[5], a[6], a[7]);

@@ -3,9 +3,9 @@ npr_dev_convert_records and npr_dev_extract_flows (HIP events around K launches 
 the host-memory npr_convert_records call (PCIe included), and the CPU oracle's convert_records
 over the same record list.  Prints one JSON line.
 
-Algorithmic bytes per record: 24 (the npr_record row) + 64 (the frame the decode reads) read,
-32 (flow row) + 32 (IPv6 side row) written for convert (Ok rows only), dense extract also 1 B of
-status.  Usage: python scripts/bench_records_api.py [--records N] [--steps K]"""
+Algorithmic bytes per record: 24 (the npr_record row) + 64 (the frame the decode reads) read;
+written: convert 32 per Ok row (+ 32 for an IPv6 flow's side row), dense extract 32 + 32 + 1 B of
+status per record.  Usage: python scripts/bench_records_api.py [--records N] [--steps K]"""
 import argparse
 import ctypes
 import json
@@ -101,7 +101,8 @@ def main():
     nm = len(fm)
     agg_mix_ms = timed_events(lambda: device.dev_flow_aggregate(fmt, f6t, n=nm, ctx=ctx, stream=stream), args.steps,
                               stream)
-    cvt_bytes = n * (24 + 64) + len(want_f) * 64
+    n6 = int(((want_f["kind"] & _abi.KIND_IPV6) != 0).sum())
+    cvt_bytes = n * (24 + 64) + len(want_f) * 32 + n6 * 32  # flow rows + side rows of IPv6 flows
     ext_bytes = n * (24 + 64 + 64 + 1)
     res = {
         "workload": f"C2 record list ({n} x 64-B frames), records + capture resident in HBM",
