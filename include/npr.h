@@ -229,8 +229,17 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   contiguous-range resident pass (one grid-wide prefix, then all rows; chained launches above
  *   ~100 MB; the default while the pipelined pass measures slower).  Same results
  *   either way.
+ * NPR_OPT_DEVICE_WINDOW (chunks, default 0 = auto): npr_parse_extract_pipelined keeps at most N
+ *   chunks of the capture (a ring, plus a 260 KiB halo for records that straddle a chunk end) and
+ *   3 links' flow rows on the device, so a host capture larger than device memory streams through
+ *   it.  N >= 3 uses the window whenever the capture has more than N chunks; 0 uses a window of 8
+ *   chunks only when staging the whole capture and its flow table would not fit in free device
+ *   memory.  Same results as the staged call, except that a record longer than the halo cannot
+ *   cross a chunk end in the window: the call then returns NPR_ERR_CAPACITY (a pcap snaplen is at
+ *   most 262144 B, which the halo covers).  Windowed chunks are at least 512 KiB.
  */
-enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4 };
+enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4,
+       NPR_OPT_DEVICE_WINDOW = 5 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);
@@ -282,7 +291,9 @@ npr_status npr_parse_extract(npr_ctx *ctx, const uint8_t *input, size_t len,
  * RIGHT-aligned, the device table's own layout: out[flow_cap - *n_flows .. flow_cap) in
  * convert_records order, so no pass moves them afterwards.  A record longer than a chunk ends a
  * link early; the call detects that and parses the staged capture again in one go.  Results
- * equal npr_parse_extract's. */
+ * equal npr_parse_extract's.  A capture larger than free device memory (or than
+ * NPR_OPT_DEVICE_WINDOW chunks) streams through a bounded device window instead of being staged
+ * whole. */
 npr_status npr_parse_extract_pipelined(npr_ctx *ctx, const uint8_t *input, size_t len,
                                        npr_global_header *header, npr_flow *out, npr_flow_v6 *out_v6,
                                        size_t flow_cap, size_t *n_flows, size_t *consumed,

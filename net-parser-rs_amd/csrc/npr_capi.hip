@@ -58,6 +58,9 @@ struct npr_ctx {
   npr_summary *sum_host = nullptr;
   uint8_t *head_h = nullptr;  // pinned: the first bytes of a large capture (link sizing)
   uint64_t sum_host_cap = 0;
+  // ... through a bounded device window (NPR_OPT_DEVICE_WINDOW): chunk ring + flow-row ring
+  int window = 0;                        // chunks (0 = auto: only when the staged capture would not fit)
+  std::vector<hipEvent_t> row_copied;    // D2H of a flow-ring slot done (the slot may be rewritten)
   std::string err;
 };
 
@@ -219,6 +222,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (c->d2h_stream) (void)hipStreamSynchronize(c->d2h_stream);
   for (hipEvent_t ev : c->copied) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : c->linked) (void)hipEventDestroy(ev);
+  for (hipEvent_t ev : c->row_copied) (void)hipEventDestroy(ev);
   if (c->sum_host) (void)hipHostFree(c->sum_host);
   if (c->head_h) (void)hipHostFree(c->head_h);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -242,6 +246,10 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
     case NPR_OPT_PIPE:  // 1: flows-only launches run the pipelined resident pass (default 0)
       if (value < 0 || value > 1) return fail(c, NPR_ERR_ARG, "NPR_OPT_PIPE must be 0 or 1");
       c->pipe = value;
+      return NPR_OK;
+    case NPR_OPT_DEVICE_WINDOW:  // chunks of the capture on the device at once (0 = auto)
+      if (value < 0 || value == 1 || value == 2) return fail(c, NPR_ERR_ARG, "NPR_OPT_DEVICE_WINDOW: 0 (auto) or >= 3 chunks");
+      c->window = value;
       return NPR_OK;
     case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first
       if (value < 0 || (value > 0 && value < 64)) return fail(c, NPR_ERR_ARG, "NPR_OPT_STREAM_CHUNK: 0 or >= 64 KiB");
@@ -730,6 +738,139 @@ static bool host_pinned(const void *p, size_t n) {
   return a.type == hipMemoryTypeHost && a.hostPointer != nullptr;
 }
 
+// ---- row f1 past device memory: the capture streams through a bounded device window --------------
+// Chunk j (file bytes [j*chunk, (j+1)*chunk)) is uploaded into ring slot j % W; kWinHalo bytes past
+// the ring's end mirror slot 0's head, so link j reads [j*chunk, (j+1)*chunk + kWinHalo) contiguously
+// from its slot (the records that straddle its chunk end).  Link j (records starting in chunk j)
+// launches once chunk j+1 has landed and writes its convert_records rows into flow-ring slot
+// j % kWinRowSlots: the kernel writes the k-th Ok flow of the capture to row flow_cap - 1 - k, so the
+// slot passed with flow_cap = S + K (K = the Ok flows before link j, read back after link j-1) gets
+// link j's rows right-aligned at its end.  The host reads each link's summary as it completes, copies
+// its rows to the caller's table on the D2H stream and launches the next link; the upload of chunk
+// j+W waits for link j.  PCIe, not the parse, sets the pace: the copy stream always holds W chunks.
+constexpr uint64_t kWinHalo = 260u << 10;  // >= 16 + 262144 B, the largest pcap snaplen's record
+constexpr uint64_t kWinRowSlots = 3;
+constexpr uint64_t kWinMinChunk = 512u << 10;
+
+static npr_status windowed_parse(npr_ctx *c, const uint8_t *in, size_t len, npr_endianness e, uint64_t chunk,
+                                 uint64_t W, npr_flow *hout, npr_flow_v6 *hout6, uint64_t fcap, npr_summary &fin) {
+  const uint64_t start = 24;
+  const uint64_t nlinks = (len + chunk - 1) / chunk;
+  const uint64_t S = chunk / 16 + 1;  // rows one link can produce: every record is >= 16 B
+  npr_status st;
+  if ((st = ensure(c, c->in, W * chunk + kWinHalo + 4096))) return st;
+  if ((st = ensure(c, c->flows, kWinRowSlots * S * sizeof(npr_flow)))) return st;
+  if (hout6 && (st = ensure(c, c->flows_v6, kWinRowSlots * S * sizeof(npr_flow_v6)))) return st;
+  if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
+  if (c->sum_host_cap < 2) {
+    if (c->sum_host) HIP_CHECK(c, hipHostFree(c->sum_host));
+    c->sum_host = nullptr;
+    c->sum_host_cap = 0;
+    HIP_CHECK(c, hipHostMalloc((void **)&c->sum_host, 2 * sizeof(npr_summary), 0));
+    c->sum_host_cap = 2;
+  }
+  if (!c->copy_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+  if (!c->d2h_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->d2h_stream, hipStreamNonBlocking));
+  if ((st = grow_events(c, c->copied, W))) return st;
+  if ((st = grow_events(c, c->linked, W))) return st;
+  if ((st = grow_events(c, c->row_copied, kWinRowSlots))) return st;
+  uint8_t *ring = (uint8_t *)c->in.p;
+  npr_flow *rows = (npr_flow *)c->flows.p;
+  npr_flow_v6 *rows6 = hout6 ? (npr_flow_v6 *)c->flows_v6.p : nullptr;
+  npr_summary *dsum = (npr_summary *)c->chain.p;
+  // links past the first do not hold the magic or the first record: their speculation context
+  // (the magic's ts_usec bound, the first record's ts_sec) comes from the host, as for a shard
+  ShardSpec sh;
+  uint32_t magic;
+  memcpy(&magic, in, 4);
+  sh.frac_max = (magic == 0xA1B2C3D4u || magic == 0xD4C3B2A1u) ? 1000000u : 1000000000u;
+  sh.has_ref = len >= start + 16;
+  sh.ts_ref = sh.has_ref ? rd_u32(in + start, e == NPR_BIG) : 0u;
+  // the compute stream's earlier work (a previous call reading the ring) comes first
+  HIP_CHECK(c, hipEventRecord(c->copied[0], c->stream));
+  HIP_CHECK(c, hipStreamWaitEvent(c->copy_stream, c->copied[0], 0));
+  HIP_CHECK(c, hipStreamWaitEvent(c->d2h_stream, c->copied[0], 0));
+  auto upload = [&](uint64_t m) -> npr_status {
+    const uint64_t a = m * chunk, b = std::min<uint64_t>(len, a + chunk);
+    HIP_CHECK(c, hipMemcpyAsync(ring + (m % W) * chunk, in + a, b - a, hipMemcpyHostToDevice, c->copy_stream));
+    if (m % W == 0)  // slot 0's head, mirrored past the ring's end for link m-1
+      HIP_CHECK(c, hipMemcpyAsync(ring + W * chunk, in + a, std::min<uint64_t>(kWinHalo, b - a), hipMemcpyHostToDevice,
+                                  c->copy_stream));
+    HIP_CHECK(c, hipEventRecord(c->copied[m % W], c->copy_stream));
+    return NPR_OK;
+  };
+  for (uint64_t m = 0; m < std::min<uint64_t>(W, nlinks); ++m)
+    if ((st = upload(m))) return st;
+  uint64_t K = 0;  // Ok flows of the links done so far
+  fin = npr_summary{};
+  for (uint64_t j = 0; j < nlinks; ++j) {
+    const uint64_t a = j * chunk, lo = std::max<uint64_t>(start, a), hi = std::min<uint64_t>(len, a + chunk);
+    const uint64_t flen = std::min<uint64_t>(len, hi + kWinHalo);  // file bytes this link may read
+    HIP_CHECK(c, hipStreamWaitEvent(c->stream, c->copied[std::min<uint64_t>(j + 1, nlinks - 1) % W], 0));
+    if (j >= kWinRowSlots) HIP_CHECK(c, hipStreamWaitEvent(c->stream, c->row_copied[j % kWinRowSlots], 0));
+    npr_dev_outputs o{};
+    o.flows = rows + (j % kWinRowSlots) * S;
+    o.flows_v6 = rows6 ? rows6 + (j % kWinRowSlots) * S : nullptr;
+    o.flow_cap = S + K;
+    o.summary = dsum + (j & 1u);
+    if (j == 0) {
+      st = launch_range(c, ring, flen, std::min(lo, hi), hi, e, 0, start, nullptr, &o, c->stream);
+    } else {
+      ShardSpec shj = sh;
+      shj.base = a;
+      st = launch_range(c, ring + (j % W) * chunk, flen, lo, hi, e, 0, NPR_NO_ENTRY, dsum + ((j - 1) & 1u), &o,
+                        c->stream, &shj);
+    }
+    if (st) return st;
+    HIP_CHECK(c, hipMemcpyAsync(c->sum_host, o.summary, sizeof(npr_summary), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(c, hipEventRecord(c->linked[j % W], c->stream));
+    if (j + W < nlinks) {  // chunk j+W reuses link j's slot
+      HIP_CHECK(c, hipStreamWaitEvent(c->copy_stream, c->linked[j % W], 0));
+      if ((st = upload(j + W))) return st;
+    }
+    HIP_CHECK(c, hipEventSynchronize(c->linked[j % W]));
+    const npr_summary sj = *c->sum_host;
+    if (sj.epoch != c->epoch) {
+      uint32_t ab = 0;
+      HIP_CHECK(c, hipMemcpy(&ab, c->abort_word, 4, hipMemcpyDeviceToHost));
+      return fail(c, NPR_ERR_TIMEOUT, "windowed parse did not complete: link %llu of %llu (epoch %u, abort word %u)",
+                  (unsigned long long)j, (unsigned long long)nlinks, c->epoch, ab);
+    }
+    // flows k in [K, min(Kj, fcap)) sit at slot rows S-1-(k-K) and belong at caller rows fcap-1-k
+    const uint64_t hk = std::min<uint64_t>(sj.n_flows, fcap);
+    if (hk > K) {
+      const uint64_t n = hk - K;
+      HIP_CHECK(c, hipStreamWaitEvent(c->d2h_stream, c->linked[j % W], 0));
+      HIP_CHECK(c, hipMemcpyAsync(hout + (fcap - hk), o.flows + (S - n), n * sizeof(npr_flow), hipMemcpyDeviceToHost,
+                                  c->d2h_stream));
+      if (hout6)
+        HIP_CHECK(c, hipMemcpyAsync(hout6 + (fcap - hk), o.flows_v6 + (S - n), n * sizeof(npr_flow_v6),
+                                    hipMemcpyDeviceToHost, c->d2h_stream));
+    }
+    HIP_CHECK(c, hipEventRecord(c->row_copied[j % kWinRowSlots], c->d2h_stream));
+    K = sj.n_flows;
+    fin = sj;
+  }
+  HIP_CHECK(c, hipStreamSynchronize(c->d2h_stream));
+  return NPR_OK;
+}
+
+// Chunks of the capture the device window holds (0 = stage the whole capture): NPR_OPT_DEVICE_WINDOW,
+// or (auto) 8 when staging the capture and its flow table would not fit in free device memory.
+static uint64_t window_chunks(npr_ctx *c, size_t len, uint64_t chunk, uint64_t fcap, bool v6) {
+  const uint64_t nlinks = (len + chunk - 1) / chunk;
+  if (c->window >= 3) return nlinks > (uint64_t)c->window ? (uint64_t)c->window : 0;
+  auto grow = [](const DevBuf &b, uint64_t want) { return want > b.cap ? want - b.cap : 0; };
+  const uint64_t need = grow(c->in, len + 16) + grow(c->flows, fcap * sizeof(npr_flow)) +
+                        (v6 ? grow(c->flows_v6, fcap * sizeof(npr_flow_v6)) : 0);
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return need > free_b / 10 * 9 && nlinks > 8 ? 8 : 0;
+}
+
 npr_status npr_parse_extract_pipelined(npr_ctx *c, const uint8_t *in, size_t len, npr_global_header *hdr,
                                        npr_flow *out, npr_flow_v6 *out_v6, size_t flow_cap, size_t *n_flows,
                                        size_t *consumed, uint64_t chunk_bytes) {
@@ -766,6 +907,22 @@ npr_status npr_parse_extract_pipelined(npr_ctx *c, const uint8_t *in, size_t len
     }
     HIP_CHECK(c, r);
     unreg.p[i] = (void *)bufs[i];
+  }
+  const uint64_t wchunk = (std::max<uint64_t>(chunk, kWinMinChunk) + 4095) & ~4095ull;
+  if (const uint64_t W = window_chunks(c, len, wchunk, fcap, out_v6 != nullptr)) {
+    npr_summary fin{};
+    if ((st = windowed_parse(c, in, len, e, wchunk, W, hout, hout6, fcap, fin))) return st;
+    if (fin.consumed + 16 <= len) {  // the chain stopped at a record: complete, yet longer than the halo?
+      const uint64_t incl = rd_u32(in + fin.consumed + 8, e == NPR_BIG);
+      if (incl <= len - fin.consumed - 16)
+        return fail(c, NPR_ERR_CAPACITY, "the record at offset %llu (%llu B) crosses a chunk end and is longer than "
+                    "the device window's %llu-B halo", (unsigned long long)fin.consumed, (unsigned long long)incl,
+                    (unsigned long long)kWinHalo);
+    }
+    if (n_flows) *n_flows = fin.n_flows;
+    if (consumed) *consumed = fin.consumed;
+    if (fin.n_flows > flow_cap || fin.flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+    return NPR_OK;
   }
   if ((st = ensure(c, c->in, len + 16))) return st;
   if ((st = ensure(c, c->flows, std::max<uint64_t>(fcap, 1) * sizeof(npr_flow)))) return st;

@@ -42,6 +42,7 @@ VXLAN_INCOMPLETE = 34
 VXLAN_INNER = 64  # + the inner frame's npr_flow_status
 VXLAN_PORT_IANA = 4789
 OPT_PIPE = 4  # npr_ctx_set_option: flows-only parses run the pipelined resident pass (1) or the contiguous one (0, default)
+OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's device window in chunks (0 auto, >= 3)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1

@@ -274,12 +274,19 @@ class PinnedArray:
             self.ptr = None
 
 
-def host_parse_extract_pipelined(data, out=None, out_v6=None, flow_cap=None, chunk_bytes=0, ctx=None):
+def host_parse_extract_pipelined(data, out=None, out_v6=None, flow_cap=None, chunk_bytes=0, ctx=None, window=None):
     """npr_parse_extract_pipelined: a host capture (numpy uint8, ideally a PinnedArray's) in, the
     convert_records flow table out on the host, transfers overlapped.  Returns (flows, flows_v6 or
-    None, n_flows, consumed): views of the right-aligned rows of `out` / `out_v6`."""
+    None, n_flows, consumed): views of the right-aligned rows of `out` / `out_v6`.  `window` (chunks,
+    >= 3) streams the capture through a bounded device window for this call (NPR_OPT_DEVICE_WINDOW)."""
     a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
     ctx = ctx or context(0)
+    if window is not None:
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_DEVICE_WINDOW, int(window)))
+        try:
+            return host_parse_extract_pipelined(a, out, out_v6, flow_cap, chunk_bytes, ctx)
+        finally:
+            ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_DEVICE_WINDOW, 0)
     cap = max((a.size - 24) // 16 + 1, 1) if flow_cap is None else flow_cap
     if out is None:
         out = np.zeros(cap, dtype=_abi.FLOW_DTYPE)

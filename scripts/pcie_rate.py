@@ -63,6 +63,24 @@ def main():
                                 "capture_GBps": round(len(blob) / t / 1e9, 2),
                                 "flows_out_GBps": round(32 * n_flows / t / 1e9, 2)}
             print(json.dumps({"run": key, **out["runs"][key]}), flush=True)
+    # the same from page-locked buffers through a bounded device window (NPR_OPT_DEVICE_WINDOW):
+    # W chunk slots + 3 flow-row slots on the device, a host sync per link
+    for mib, win in ((8, 4), (8, 8), (32, 3), (32, 8)):
+        run = lambda: device.host_parse_extract_pipelined(pin_in.array, pin_out.array, None, cap, mib << 20, ctx=ctx,
+                                                          window=win)
+        run()
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            flows, _, n_flows, consumed = run()
+            ts.append(time.perf_counter() - t0)
+        t = min(ts)
+        key = f"windowed_pinned_{mib}MiB_x{win}"
+        out["runs"][key] = {"s": round(t, 5), "Mpackets_per_s": round(n / t / 1e6, 1),
+                            "capture_GBps": round(len(blob) / t / 1e9, 2),
+                            "flows_out_GBps": round(32 * n_flows / t / 1e9, 2),
+                            "device_window_MB": round((win * (mib << 20) + (260 << 10)) / 1e6, 1)}
+        print(json.dumps({"run": key, **out["runs"][key]}), flush=True)
     # the raw link: one pinned H2D of the capture, one pinned D2H of the flow table
     import torch
     d = torch.empty(len(blob), dtype=torch.uint8, device="cuda")

@@ -127,3 +127,92 @@ def test_pipelined_host_parse_pinned_buffers(corpus):
 def test_pipelined_c2_x4_320mb():
     """The measured configuration: 4M C2 records, 32 MiB chunks, bit-exact."""
     check_pipelined(synth.fixed64(4_000_000), 0, pinned=True)
+
+
+# ---- the bounded device window (NPR_OPT_DEVICE_WINDOW): captures larger than device memory ----
+WINDOW_CORPORA = {  # each larger than 3 windowed chunks of 512 KiB
+    "c2": lambda: synth.fixed64(100_000),
+    "c3": lambda: synth.variable_mix(6_000),
+    "quirk_big_endian": lambda: synth.quirk_corpus(40_000, seed=62, big=True),
+    "adversarial": lambda: synth.quirk_corpus(6_000, seed=63, fake_every=3, zero_every=7, jumbo_every=150),
+    "truncated_payload": lambda: synth.quirk_corpus(30_000, seed=65, tail="truncated_payload"),
+    "huge_incl": lambda: synth.quirk_corpus(30_000, seed=66, tail="huge_incl"),
+    "corrupt_incl_mid_file": lambda: synth.corrupt_midfile(synth.fixed64(60_000), at_record=41_234),
+}
+
+
+def check_windowed(blob, chunk_bytes, window, pinned=False):
+    """npr_parse_extract_pipelined through a ring of `window` chunk slots (plus the halo mirror)
+    and three flow-row slots, against the oracle; flows right-aligned in the caller's table."""
+    rc, ohdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
+    want_flows, want_v6 = _oracle.convert_records(blob, want_recs)
+    cap = len(want_recs) + 5
+    if pinned:
+        src = device.PinnedArray(len(blob))
+        src.array[:] = np.frombuffer(blob, dtype=np.uint8)
+        a = src.array
+    else:
+        a = np.frombuffer(blob, dtype=np.uint8).copy()
+    out, out6 = np.zeros(cap, _abi.FLOW_DTYPE), np.zeros(cap, _abi.FLOW_V6_DTYPE)
+    try:
+        flows, v6, n_flows, consumed = device.host_parse_extract_pipelined(a, out, out6, cap, chunk_bytes,
+                                                                           window=window)
+    finally:
+        if pinned:
+            src.close()
+    assert (n_flows, consumed) == (len(want_flows), want_cons)
+    assert flows.tobytes() == want_flows.tobytes()
+    assert not out[:cap - n_flows].view(np.uint8).any()  # nothing written left of the flows
+    m = (want_flows["kind"] & _abi.KIND_IPV6) != 0
+    assert v6[m].tobytes() == want_v6[m].tobytes()
+    return n_flows, consumed
+
+
+@pytest.mark.parametrize("window", [3, 5])
+@pytest.mark.parametrize("corpus", sorted(WINDOW_CORPORA))
+def test_windowed_pipelined_matches_oracle(corpus, window):
+    check_windowed(WINDOW_CORPORA[corpus](), 1 << 19, window)
+
+
+def test_windowed_chunks_not_a_multiple_of_the_tile():
+    """A requested chunk is rounded up to 4 KiB and to the 512 KiB minimum."""
+    check_windowed(synth.variable_mix(3_000), 600_001, 3, pinned=True)
+
+
+def test_windowed_c2_x4_320mb():
+    """4M C2 records (320 MB) through 8 slots of 32 MiB: the default chunk, bit-exact."""
+    check_windowed(synth.fixed64(4_000_000), 0, 8, pinned=True)
+
+
+def _with_long_record(incl, at_byte):
+    """C2 records, then one record of `incl` payload bytes starting near `at_byte`, then more."""
+    head = np.frombuffer(synth.fixed64((at_byte - 24) // 80), dtype=np.uint8)
+    tail = np.frombuffer(synth.fixed64(20_000), dtype=np.uint8)[24:]
+    rec = np.zeros(16 + incl, dtype=np.uint8)
+    rec[:16] = np.frombuffer(head[24:40].tobytes(), dtype=np.uint8)  # the first record's timestamps
+    rec[8:12] = np.frombuffer(np.uint32(incl).tobytes(), dtype=np.uint8)
+    rec[12:16] = rec[8:12]
+    rec[16:] = np.frombuffer(head[40:104].tobytes() * (incl // 64 + 1), dtype=np.uint8)[:incl]
+    return np.concatenate([head, rec, tail]).tobytes()
+
+
+def test_windowed_record_longer_than_the_halo():
+    """A 300 KB record across a chunk end does not fit the window's 260 KiB halo: the windowed call
+    says so (NPR_ERR_CAPACITY) instead of stopping the chain there; the staged call parses it."""
+    blob = _with_long_record(300_000, (1 << 19) - 8_000)
+    with pytest.raises(npr.DeviceError, match="halo"):
+        device.host_parse_extract_pipelined(np.frombuffer(blob, dtype=np.uint8).copy(), chunk_bytes=1 << 19, window=3)
+    check_pipelined(blob, 1 << 19, pinned=False)
+
+
+def test_windowed_record_within_the_halo():
+    """A 250 KB record across a chunk end is read from the next slot's mirror / halo."""
+    check_windowed(_with_long_record(250_000, 3 * (1 << 19) - 8_000), 1 << 19, 3)
+
+
+def test_device_window_option_values():
+    ctx = npr.context(0)
+    for bad in (-1, 1, 2):
+        assert ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_DEVICE_WINDOW, bad) == _abi.ERR_ARG
+    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_DEVICE_WINDOW, 3))
+    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_DEVICE_WINDOW, 0))
