@@ -21,10 +21,11 @@
 //   k_count_tiles + k_emit_tiles (record-table launches): two streaming passes of one-wave
 //     workgroups, one per tile; pass 1 publishes A and folds 64-tile groups, pass 2 rebuilds the
 //     exact state before each tile from the folds and writes every record row and flow;
-//   k_parse_resident (flows-only launches, NPR_PIPE=0): persistent waves, each owning a
+//   k_parse_resident (flows-only launches, the default): persistent waves, each owning a
 //     contiguous tile range, flows kept in registers; one pass with a decoupled look-back over
-//     16-wave workgroup aggregates;
-//   k_parse_pipe (flows-only launches, default): persistent workgroups of 15 parser waves + 1
+//     16-wave workgroup aggregates (chained launches for captures past what registers hold);
+//   k_parse_pipe (flows-only launches, opt-in NPR_OPT_PIPE / NPR_PIPE=1; measured slower):
+//     persistent workgroups of 15 parser waves + 1
 //     resolver wave; tiles are dealt round-robin (tile = round * parsers + parser), so every
 //     round is a contiguous slab of the capture; the resolver folds each round's aggregates and
 //     posts every parser's exact prefix while the parsers stream on (npr_kernels_pipe.inc).

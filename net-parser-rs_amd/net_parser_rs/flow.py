@@ -124,10 +124,15 @@ def convert_records(records):
         k = ctypes.c_size_t(0)
         ctx.check(ctx.lib.npr_convert_records(ctx.handle, a.ctypes.data if a.size else None, a.size, t.ctypes.data,
                                               n, flows.ctypes.data, v6.ctypes.data, n, ctypes.byref(k)))
-        by_off = {r.offset: r for r in records}
+        # rows are the Ok records in reverse list order: pair each with the next record (walking the
+        # list backwards) at its offset, so a record listed twice yields two pairs, as in the reference
+        j = n - 1
         for i in range(k.value):
             f = Flow._from_row(flows[i], v6[i])
-            out.append((by_off[f.record_offset], f))
+            while records[j].offset != f.record_offset:
+                j -= 1
+            out.append((records[j], f))
+            j -= 1
         return out
     for r in reversed(records):
         try:

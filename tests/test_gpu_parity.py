@@ -280,6 +280,25 @@ def test_mirror_api_matches_oracle():
     assert len(recs_list) == len(recs)
 
 
+def test_mirror_convert_records_keeps_repeated_records():
+    """convert_records(Vec<PcapRecord>) pops every element (src/flow/mod.rs:101-123): a record listed
+    twice yields two (record, flow) pairs, each paired with its own list element."""
+    blob = synth.quirk_corpus(500, seed=18)
+    _, f = npr.parse(blob)
+    rs = f.records.into_inner()
+    lst = rs[:40] + rs[10:20] + rs[5:6] + rs[300:]
+    pairs = npr.flow.convert_records(lst)
+    want = []
+    for r in reversed(lst):
+        try:
+            want.append((r, r.extract_flow()))
+        except npr.flow.FlowError:
+            pass
+    assert len(pairs) == len(want)
+    for (r, fl), (wr, wfl) in zip(pairs, want):
+        assert r is wr and fl == wfl
+
+
 # ---- chained launches (npr_dev_parse_extract_chunked): the capture parsed chunk after chunk --------
 def check_chunked(blob, chunk, start=24, endianness=None):
     if start == 24:
