@@ -891,9 +891,56 @@ __device__ __forceinline__ uint32_t incl_at(const uint32_t *w, uint32_t r) {
 // length as the previous one, or longer than a tile).  hop_span is 0 unless every record starting
 // inside the tile with incl <= kTile ends inside the capture, so no Incomplete test is needed
 // here.  Returns the next position.
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {  // byte address in LDS of an LDS pointer
+  return (uint32_t)(uintptr_t)((__attribute__((address_space(3))) const void *)p);
+}
 template <bool BIG>
 __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, uint32_t r, uint32_t incl,
                                             uint32_t hop_span, uint32_t &n, uint32_t &last) {
+#ifndef NPR_HOP_CXX
+  // The loop by hand (the compiled one spent ~17 SALU per hop on flow blocks and copies): per hop
+  // one broadcast ds_write_b16 of the offset, two ds_read_b32 of the next header's incl_len word
+  // pair, v_alignbyte + readfirstlane, and three compare-and-branch exits; the srec address walks
+  // in a VGPR.  Both LDS pointers come from __shared__ arrays (every walk_tile caller's).
+  uint32_t va, vd, vlo, vhi, t;
+  const uint32_t sa = lds_addr(srec) + 2u * n, wb = lds_addr(w);
+#define NPR_HOP_ASM(PERM)                                                                              \
+  asm volatile(                                                                                        \
+      "v_mov_b32 %[va], %[sa]\n"                                                                       \
+      "1:\n\t"                                                                        \
+      "v_mov_b32 %[vd], %[r]\n\t"                                                                      \
+      "ds_write_b16 %[va], %[vd]\n\t"                                                                  \
+      "v_add_u32 %[va], 2, %[va]\n\t"                                                                  \
+      "s_add_u32 %[n], %[n], 1\n\t"                                                                    \
+      "s_add_u32 %[r], %[r], %[incl]\n\t"                                                              \
+      "s_add_u32 %[r], %[r], 16\n\t"                                                                   \
+      "s_mov_b32 %[last], %[incl]\n\t"                                                                 \
+      "s_cmp_ge_u32 %[r], %[span]\n\t"                                                                 \
+      "s_cbranch_scc1 2f\n\t"                                                          \
+      "s_and_b32 %[t], %[r], -4\n\t"                                                                   \
+      "s_add_u32 %[t], %[t], %[wb]\n\t"                                                                \
+      "v_mov_b32 %[vlo], %[t]\n\t"                                                                     \
+      "ds_read_b32 %[vhi], %[vlo] offset:12\n\t"                                                       \
+      "ds_read_b32 %[vlo], %[vlo] offset:8\n\t"                                                        \
+      "s_and_b32 %[t], %[r], 3\n\t"                                                                    \
+      "s_waitcnt lgkmcnt(0)\n\t"                                                                       \
+      "v_alignbyte_b32 %[vlo], %[vhi], %[vlo], %[t]\n\t" PERM                                          \
+      "s_nop 0\n\t"                                                                                    \
+      "v_readfirstlane_b32 %[incl], %[vlo]\n\t"                                                        \
+      "s_cmp_eq_u32 %[incl], %[last]\n\t"                                                              \
+      "s_cbranch_scc1 2f\n\t"                                                          \
+      "s_cmpk_le_u32 %[incl], %[tile]\n\t"                                                             \
+      "s_cbranch_scc1 1b\n"                                                             \
+      "2:"                                                                             \
+      : [r] "+s"(r), [n] "+s"(n), [incl] "+s"(incl), [last] "=&s"(last), [t] "=&s"(t), [va] "=&v"(va),  \
+        [vd] "=&v"(vd), [vlo] "=&v"(vlo), [vhi] "=&v"(vhi)                                             \
+      : [sa] "s"(sa), [wb] "s"(wb), [span] "s"(hop_span), [perm] "s"(0x00010203u), [tile] "i"(kTile)  \
+      : "scc", "memory")
+  if constexpr (BIG) NPR_HOP_ASM("v_perm_b32 %[vlo], 0, %[vlo], %[perm]\n\t");
+  else NPR_HOP_ASM("");
+#undef NPR_HOP_ASM
+  return r;
+#else
   for (;;) {
     srec[n] = (uint16_t)r;
     ++n;
@@ -909,6 +956,7 @@ __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, u
     if (d > (uint32_t)kTile) break;
   }
   return r;
+#endif
 }
 
 __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
