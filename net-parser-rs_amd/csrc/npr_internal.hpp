@@ -11,7 +11,7 @@ namespace npr {
 
 // Tile geometry of the parse+extract kernels: ONE WAVE per tile.
 constexpr int kBlock = 256;            // workgroup size of the auxiliary kernels (dense extract, compaction)
-constexpr int kWave = 64;              // the parse kernels: one-wave workgroups
+constexpr int kWave = 64;              // lanes per wave (the two-pass kernels: one-wave workgroups)
 #ifndef NPR_TILE_BYTES
 #define NPR_TILE_BYTES 4096
 #endif
@@ -49,7 +49,7 @@ struct alignas(128) GroupSlot {
 struct alignas(128) RangeSlot {
   uint64_t a[4];
   uint64_t p[3];
-  uint64_t e[5];  // exclusive prefix inside its 64-wave group (kPre* words), by the group's fold
+  uint64_t e[5];  // unused by the resident pass (kept: RangeSlot and TileSlot share one layout)
   uint64_t pad[4];
 };
 static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
@@ -133,7 +133,8 @@ struct ParseParams {
 };
 
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)
-// k_parse_resident, one launch of p.nwaves one-wave workgroups.
+// k_parse_resident, one launch of p.nwaves persistent waves in 16-wave workgroups (p.pipe:
+// k_parse_pipe, 15 parser waves + 1 resolver per workgroup).
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
 // resident waves per CU the hardware admits for k_parse_resident / k_parse_pipe (occupancy query)
 int resident_waves_per_cu();

@@ -1459,21 +1459,26 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
 // =============================================================================================
 // RESIDENT SINGLE PASS — k_parse_resident (flows-only launches: the `extract` bench's output)
 //
-// ONE launch of W persistent one-wave workgroups; wave v owns the contiguous tile range
-// [c0(v), c1(v)).  Every byte of the capture is read once:
-//   phase A: the range streams through a per-wave LDS ring (LDS-DMA); the chain is speculated
-//     ONCE, at the range's first tile (wave 0: `start`), then walked tile to tile; every record
-//     is decoded with its fields and the Ok flows of each 64-record round are KEPT IN REGISTERS
-//     (kResSlots rounds; later rounds are deferred to phase B).  The wave publishes its range
-//     aggregate A(v) = {exit, entry, records, Ok flows}; the last wave of each 64-wave group
-//     folds the group's aggregates into G1 (chain-consistency monoid, as for tiles).
-//   phase B: the exact chain state before v = anchor ⊕ G1(groups before) ⊕ A(waves before, in
-//     this group): two 64-wide windows, all produced by LOWER-indexed waves (dispatched
-//     earlier: resident or done, so no co-residency is assumed).  When v's speculated entry is
-//     the exact position (the common case), the register-held flows go straight to their
-//     convert_records rows and only deferred tiles are re-read; otherwise the range is re-walked
-//     from the exact position.  A contradiction below v waits for the offending wave's exact
-//     prefix P(m), published at the end of its own phase B.
+// ONE launch of W persistent waves in workgroups of kResWg (16: one workgroup per CU, 4 waves per
+// SIMD); wave v = b * kResWg + wid owns the contiguous tile range [c0(v), c1(v)).  Every byte of
+// the capture is read once:
+//   phase A: the range streams through a two-slot LDS ring per wave (LDS-DMA, the next tile in
+//     flight while the current one is parsed); the chain is speculated ONCE, at the range's first
+//     tile (wave 0: `start`), then walked tile to tile (stride speculation for repeating lengths,
+//     hop_run for variable ones); every record is decoded with its fields and the Ok flows of each
+//     64-record round are KEPT IN REGISTERS (kResSlots rounds; PACK: sparse tiles share the last
+//     round; later rounds are deferred to phase B).  The wave's range aggregate A(v) = {exit,
+//     entry, records, Ok flows} goes to LDS (and to its RangeSlot for the rare generic prefix).
+//   the prefix: wave 0 folds the workgroup's 16 A's in LDS (chain-consistency monoid), publishes
+//     the workgroup aggregate G(b) and looks back over G(0..b-1) of the LOWER workgroups (all
+//     windows loaded at once, only unpublished lanes re-read by returning atomics with backed-off
+//     naps): E(b) = anchor (or the previous link's summary) ⊕ G(0) ⊕ ... ⊕ G(b-1), then each
+//     wave's prefix X(v) = E(b) ⊕ A(waves before v in b) in LDS.  All workgroups are co-resident
+//     (the host sizes the grid by the occupancy query) and every wait is bounded.
+//   phase B: when X(v).exit is v's speculated entry (the common case), the register-held flows go
+//     straight to their convert_records rows flow_cap - 1 - (X.ok + rank) and only deferred tiles
+//     are re-read; otherwise the range is re-walked from the exact position.  A contradiction below
+//     v waits for the offending wave's exact prefix P(m), published at the end of its own phase B.
 // =============================================================================================
 #ifndef NPR_RES_RING
 #define NPR_RES_RING 2
