@@ -242,7 +242,16 @@ def run_sharded(args, dev, local, rank, world):
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     # C4 frames are IPv4 by construction: no IPv6 side table to move (pass ws.flows_v6 rows otherwise)
-    step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000)
+    # the per-step 64-B summaries are exchanged on the host (gloo over loopback: one node), off the
+    # GPU timeline; without gloo the same step all-gathers them over RCCL between two parses
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    try:
+        meta = dist.new_group(backend="gloo")
+    except RuntimeError as e:
+        print(f"[rank {rank}] no gloo group ({e}); summaries over RCCL", file=sys.stderr, flush=True)
+        meta = None
+    step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000,
+                                       meta_group=meta)
     metas, live, rounds = step.step()
     _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
     assert rounds == 1 and r_tot == n_total and f_tot == n_total, (rounds, r_tot, f_tot)
@@ -251,8 +260,15 @@ def run_sharded(args, dev, local, rank, world):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    # two steps in flight: step k's host replay of the exchanged summaries runs while step k+1 parses
     for _ in range(args.steps):
-        step.step()
+        step.launch_step()
+        if len(step.pending) > 1:
+            _, _, r = step.finish_step()
+            rounds = max(rounds, r)
+    while step.pending:
+        _, _, r = step.finish_step()
+        rounds = max(rounds, r)
     torch.cuda.synchronize()
     dist.barrier()
     wall = time.perf_counter() - t0
@@ -292,7 +308,9 @@ def run_sharded(args, dev, local, rank, world):
     out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
     out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
     step_ms = wall * 1e3 / args.steps
-    out["exchange"] = {"collective": "RCCL all_gather of device summaries (one per step)", "rounds": rounds}
+    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per step, "
+                                      "overlapped with the next step's parse; RCCL carries the flow rows") if meta is not None
+                       else "RCCL all_gather of the ranks' device summaries, one per step", "rounds": rounds}
     out["gather_ms"] = round(gather_ms, 3)
     out["gather"] = ("RCCL point-to-point of every rank's flow rows straight into rank 0's merged "
                      f"convert_records table ({32 * n_total / 1e9:.2f} GB)")
@@ -301,6 +319,11 @@ def run_sharded(args, dev, local, rank, world):
 
 
 def main():
+    # the one JSON line goes to the original stdout; everything else written to fd 1 (e.g. the RCCL
+    # version banner of communicator init) goes to stderr
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    json_out = os.fdopen(out_fd, "w")
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -314,6 +337,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gate", action="store_true", help=argparse.SUPPRESS)  # ablation builds only
     ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
+    ap.add_argument("--sharded", action="store_true",
+                    help="c4 through the multi-GPU step (RCCL exchange + gather) even at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -321,19 +346,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config is None:
         args.config = "c2" if world == 1 else "c4"
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    sharded = world > 1 or args.sharded
+    if sharded:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if sharded:
         if args.config != "c4":
             raise SystemExit("N > 1 runs the sharded C4 workload (--config c4)")
         out = run_sharded(args, dev, local, rank, world)
     else:
         out = run_single(args, dev, local)
     if rank == 0:
-        print(json.dumps(out), flush=True)
-    if world > 1:
+        print(json.dumps(out), file=json_out, flush=True)
+    if sharded:
         dist.destroy_process_group()
 
 

@@ -85,6 +85,14 @@ class Workspace:
         self.ctx.check(st)
         self._stream = s
 
+    def use_summary(self, summary):
+        """Launches from now on write their npr_summary into `summary`: 64 uint8 on this device, or in
+        page-locked host memory (the last launch of a parse then stores it straight over PCIe, so the
+        host reads it after an event, with no copy kernel behind the parse)."""
+        assert (summary.is_cuda or summary.is_pinned()) and summary.dtype == torch.uint8 and summary.numel() >= 64
+        self.summary = summary
+        self.outs.summary = summary.data_ptr()
+
     def flow_rows(self, n_flows=None):
         """The right-aligned flow rows as device tensors (views, no copy): (flows, flows_v6)."""
         k = min(self.last.n_flows if n_flows is None else int(n_flows), self.flow_cap)

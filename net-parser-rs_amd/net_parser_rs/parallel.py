@@ -302,7 +302,7 @@ class DeviceShardedParse:
     [base, base + nbytes)."""
 
     def __init__(self, ws, buf, base, bounds, file_len, endianness=_abi.LITTLE, usec_magic=True, ts_ref=None,
-                 start=24, group=None, nbytes=None, chunk_bytes=0):
+                 start=24, group=None, nbytes=None, chunk_bytes=0, meta_group=None):
         import torch
         import torch.distributed as dist
         self.ws, self.buf, self.base, self.bounds = ws, buf, int(base), bounds
@@ -312,6 +312,23 @@ class DeviceShardedParse:
         self.chunk = int(chunk_bytes)
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.gathered = torch.zeros(self.world * ws.summary.numel(), dtype=torch.uint8, device=ws.summary.device)
+        # launch_step / finish_step: two exchanges in flight (device + page-locked host copies)
+        pin = ws.summary.device.type == "cuda"
+        self._g2 = [torch.zeros_like(self.gathered) for _ in range(2)]
+        self._h2 = [torch.zeros(self.gathered.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
+        self._ev2 = [torch.cuda.Event() if pin else None for _ in range(2)]
+        self._k = 0
+        self.pending = []
+        # meta_group (a gloo group over the same ranks): launch_step's exchange moves the 64-B
+        # summaries on the HOST instead (D2H on a side stream, all-gathered in finish_step), so no
+        # collective kernel or stream join sits between two parses; the flow rows still go over RCCL
+        self.meta_group = meta_group
+        if meta_group is not None:
+            # the parse's last link stores its summary straight into page-locked host memory: the
+            # host waits for an event behind the parse, no copy kernel needs a CU the next parse holds
+            self._sum2 = [torch.zeros(ws.summary.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
+            self._gh = torch.zeros(self.gathered.numel(), dtype=torch.uint8)
+            self._bind(self._sum2[0])
 
     def _launch(self, start, speculative):
         lo, hi = self.bounds[self.rank]
@@ -319,15 +336,81 @@ class DeviceShardedParse:
         self.ws.launch_shard(self.buf, self.base, start, hi, endianness=self.e, speculative=speculative,
                              usec_magic=self.usec, ts_ref=self.ts_ref, chunk_bytes=self.chunk, nbytes=self.nbytes)
 
-    def _exchange(self):
-        import torch.distributed as dist
-        dist.all_gather_into_tensor(self.gathered, self.ws.summary, group=self.group)
-        g = self.gathered.cpu().numpy().reshape(self.world, -1)[:, :40].copy().view(_abi.SUMMARY_DTYPE).reshape(-1)
+    def _metas(self, host_bytes):
+        g = host_bytes.numpy().reshape(self.world, -1)[:, :40].copy().view(_abi.SUMMARY_DTYPE).reshape(-1)
         if (g["epoch"] == 0).any() or (g["flags"] != 0).any():
             bad = [int(r) for r in range(self.world) if g["epoch"][r] == 0 or g["flags"][r] != 0]
             raise RuntimeError(f"shard parse did not complete or overflowed on ranks {bad}")
         return [ShardResult(entry=int(x["entry"]), consumed=int(x["consumed"]), n_records=int(x["n_records"]),
                             n_flows=int(x["n_flows"])) for x in g]
+
+    def _bind(self, summary):
+        if hasattr(self.ws, "use_summary"):
+            self.ws.use_summary(summary)
+        else:
+            self.ws.summary = summary
+
+    def _exchange(self):
+        import torch
+        import torch.distributed as dist
+        if self.meta_group is not None:  # the summary is in host memory: wait for the parse, gather on the host
+            if torch.cuda.is_available():
+                torch.cuda.current_stream().synchronize()
+            dist.all_gather(list(self._gh.view(self.world, -1).unbind(0)), self.ws.summary, group=self.meta_group)
+            return self._metas(self._gh)
+        dist.all_gather_into_tensor(self.gathered, self.ws.summary, group=self.group)
+        return self._metas(self.gathered.cpu())
+
+    def launch_step(self):
+        """The step's device work without waiting for it: this rank's parse from its speculated (or
+        known) start, the all-gather of the summaries and their copy to page-locked host memory,
+        all stream-ordered.  finish_step() replays the chain on the host, so the host work of step k
+        overlaps the parse of step k+1 (at most two steps in flight: the exchange buffers alternate)."""
+        import torch.distributed as dist
+        if len(self.pending) >= 2:
+            raise RuntimeError("finish_step() the oldest step first")
+        import torch
+        lo, hi = self.bounds[self.rank]
+        i = self._k & 1
+        self._k += 1
+        if self.meta_group is not None:
+            self._bind(self._sum2[i])
+            self._launch(self.start if self.rank == 0 else lo, self.rank > 0)
+            if self._ev2[i] is not None:
+                self._ev2[i].record()
+        else:
+            self._launch(self.start if self.rank == 0 else lo, self.rank > 0)
+            dist.all_gather_into_tensor(self._g2[i], self.ws.summary, group=self.group)
+            self._h2[i].copy_(self._g2[i], non_blocking=True)
+            if self._ev2[i] is not None:
+                self._ev2[i].record()
+        self.pending.append(i)
+
+    def finish_step(self):
+        """-> (metas, live, rounds) of the oldest launch_step().  A contradicted speculation (never on
+        C4) drains the device and runs the whole step again synchronously (every rank decides the
+        same from the same summaries, so the collectives stay matched)."""
+        import torch
+        import torch.distributed as dist
+        i = self.pending.pop(0)
+        if self._ev2[i] is not None:
+            self._ev2[i].synchronize()
+        if self.meta_group is not None:  # the summaries' all-gather on the host (gloo)
+            dist.all_gather(list(self._h2[i].view(self.world, -1).unbind(0)), self._sum2[i], group=self.meta_group)
+        metas = self._metas(self._h2[i])
+        bad, e, live = replay(self.start, self.bounds, metas)
+        if bad is not None:
+            if torch.cuda.is_available():
+                torch.cuda.synchronize()
+            while self.pending:  # later steps parsed from the same speculation: redone below
+                self.pending.pop(0)
+            return self.step()
+        lo, hi = self.bounds[self.rank]
+        m = metas[self.rank]
+        if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
+            raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
+        self.metas, self.live = metas, live
+        return metas, live, 1
 
     def step(self):
         """-> (metas, live, rounds).  Raises HaloError when a chain stops short of a buffer end."""

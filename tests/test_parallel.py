@@ -212,7 +212,7 @@ class OracleShardWorkspace:
         return self.flows[lo:], self.flows_v6[lo:]
 
 
-def _step_rank_main(rank, world, port, blob, wrong, q):
+def _step_rank_main(rank, world, port, blob, wrong, q, pipelined=False):
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -225,8 +225,20 @@ def _step_rank_main(rank, world, port, blob, wrong, q):
         shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
         spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
         ws = OracleShardWorkspace(len(recs) + 1, spec)
-        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
-        metas, live, rounds = step.step()
+        meta = dist.new_group(backend="gloo") if pipelined == "host_meta" else None
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), meta_group=meta)
+        if pipelined:  # the bench's timed loop: two steps in flight, host replay of step k during step k+1
+            rounds = 0
+            for _ in range(3):
+                step.launch_step()
+                if len(step.pending) > 1:
+                    metas, live, r = step.finish_step()
+                    rounds = max(rounds, r)
+            while step.pending:
+                metas, live, r = step.finish_step()
+                rounds = max(rounds, r)
+        else:
+            metas, live, rounds = step.step()
         fl, f6 = step.rows()
         merged, merged6 = parallel.gather_flow_tables(fl, f6, metas, live)
         if rank == 0:
@@ -239,8 +251,9 @@ def _step_rank_main(rank, world, port, blob, wrong, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("pipelined", [False, True, "host_meta"], ids=["step", "launch_finish", "host_meta"])
 @pytest.mark.parametrize("wrong", [False, True], ids=["exact", "rerun"])
-def test_gloo_world2_device_step_protocol(wrong):
+def test_gloo_world2_device_step_protocol(wrong, pipelined):
     """DeviceShardedParse (the bench's multi-GPU step) + gather_flow_tables over gloo: each rank holds
     only its shard's bytes; summaries all-gathered, the chain replayed, a wrong speculated start
     re-parsed, flow rows sent point-to-point into the root's merged table."""
@@ -248,7 +261,7 @@ def test_gloo_world2_device_step_protocol(wrong):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_step_rank_main, args=(r, 2, port, blob, wrong, q)) for r in range(2)]
+    procs = [ctx.Process(target=_step_rank_main, args=(r, 2, port, blob, wrong, q, pipelined)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
