@@ -188,3 +188,63 @@ def test_fresh_context_slot_sizing(records):
     sm = ws.check()
     assert (sm.n_records, sm.consumed) == (len(recs), cons)
     assert ws.flows_np().tobytes() == flows.tobytes()
+
+
+def test_summary_in_page_locked_host_memory():
+    """Workspace.use_summary(page-locked host tensor): the parse's last link stores the summary
+    straight over PCIe (the multi-GPU step reads it after an event, no copy kernel); it equals the
+    device summary of the same parse, over a chained (multi-link) capture too."""
+    stream = torch.cuda.Stream()  # launches and the event on one explicit stream (NULL = the context's own)
+    torch.cuda.set_stream(stream)
+    for blob in (synth.fixed64(300_000), synth.variable_mix(200_000)):
+        buf = to_dev(blob)
+        ws = device.Workspace(record_cap=1, flow_cap=len(blob) // 80 + 1, records=False, flows=True, flows_v6=False)
+        ws.launch_chunked(buf, chunk_bytes=4 << 20)
+        want = ws.check()
+        host = torch.zeros(64, dtype=torch.uint8, pin_memory=True)
+        ws.use_summary(host)
+        ev = torch.cuda.Event()
+        ws.launch_chunked(buf, chunk_bytes=4 << 20)
+        ev.record()
+        ev.synchronize()
+        got = host[:40].numpy().copy().view(_abi.SUMMARY_DTYPE)[0]
+        assert (int(got["n_records"]), int(got["n_flows"]), int(got["consumed"])) == \
+            (want.n_records, want.n_flows, want.consumed)
+        assert int(got["epoch"]) != 0 and int(got["flags"]) == 0
+    torch.cuda.set_stream(torch.cuda.default_stream())
+
+
+def test_device_step_two_in_flight_world1():
+    """DeviceShardedParse's launch_step / finish_step with the summaries in host memory and a gloo
+    metadata group (the bench's multi-GPU loop), at world size 1 on the GPU: three steps in flight,
+    then the rows byte-compared with the oracle."""
+    import os
+    import socket
+    import torch.distributed as dist
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    torch.cuda.set_stream(torch.cuda.Stream())  # as bench.py: an explicit stream (NULL = the context's own)
+    try:
+        blob = synth.fixed64(400_000)
+        buf = to_dev(blob)
+        n = 400_000
+        ws = device.Workspace(record_cap=1, flow_cap=n, records=False, flows=True, flows_v6=False)
+        step = parallel.DeviceShardedParse(ws, buf, 0, [(24, len(blob))], len(blob), usec_magic=True,
+                                           meta_group=dist.group.WORLD)
+        for _ in range(3):
+            step.launch_step()
+            if len(step.pending) > 1:
+                step.finish_step()
+        while step.pending:
+            metas, live, rounds = step.finish_step()
+        assert rounds == 1 and metas[0].n_records == n and metas[0].n_flows == n
+        fl, _ = step.rows()
+        want = oracle_flows(blob)[3]
+        assert fl.cpu().numpy().tobytes() == want.tobytes()
+    finally:
+        torch.cuda.set_stream(torch.cuda.default_stream())
+        dist.destroy_process_group()
