@@ -275,3 +275,4 @@ class CaptureParser:
 
 
 from . import flow  # noqa: E402  (flow needs the classes above)
+from . import layers  # noqa: E402
