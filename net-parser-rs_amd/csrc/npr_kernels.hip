@@ -2121,13 +2121,14 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
         entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
         E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
       }
-#ifdef NPR_EXP_NOFOLD  // ablation (timing only: wrong row positions): the exit of G(b-1), no fold
+#ifdef NPR_EXP_NOFOLD  // ablation (timing only, C2's fixed 80-B records): E from G(b-1)'s exit, no fold
       if (b > 0 && okw) {
         uint64_t ex = 0;
 #pragma unroll
         for (int w = 0; w < kTopWin; ++w)
           if (64u * (uint32_t)w < b) ex = rl64(G[w].exit, 0);
         E.exit = ex;
+        E.cnt = E.ok = (ex - kp.start) / 80u;  // exact for C2's 80-B records only: rows land where they belong
         E.last = sh.a[0].first - 1;
       }
 #else
