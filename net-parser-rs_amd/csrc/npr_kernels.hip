@@ -1769,12 +1769,17 @@ __device__ __forceinline__ void st_wt16(uint32_t *p, u32x4 v) {
 }
 
 // one Ok flow row (+ its IPv6 side row, re-read from the capture at the decoded offset)
+__device__ __forceinline__ void res_put_v6(const ParseParams &kp, uint64_t o, const uint32_t (&s)[8], uint64_t p);
 __device__ __forceinline__ void res_put(const ParseParams &kp, uint64_t o, const uint32_t (&s)[8], uint64_t p) {
   const bool v6 = (s[6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
   uint32_t *d = kp.flows + o * 8;
   st_wt16(d, u32x4{v6 ? 0u : s[0], v6 ? 0u : s[1], s[2], s[3]});
   st_wt16(d + 4, u32x4{s[4], s[5], s[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)});
-  if (v6 && kp.flows_v6) {
+  if (v6) res_put_v6(kp, o, s, p);
+}
+// the IPv6 side row of an IPv6 flow (its 32-B address block re-read from the capture)
+__device__ __forceinline__ void res_put_v6(const ParseParams &kp, uint64_t o, const uint32_t (&s)[8], uint64_t p) {
+  if (kp.flows_v6) {
     const uint64_t a = p + 16 + s[0];  // the 32-B address block: 9 aligned dwords + alignbyte
     const uint64_t al = a & ~3ull;
     const uint64_t room = kp.len - al;
@@ -2172,10 +2177,46 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
             const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
             const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
                                  (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
+#ifndef NPR_ROWS_PER_LANE
+            // The round's Ok rows are one contiguous block of nok rows: stage them in this wave's idle
+            // ring slot in address order, then store the block as contiguous 16-B chunks (lane i:
+            // chunks i and 64 + i), so each store instruction writes whole lines.  A write-only
+            // microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane rounds
+            // (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s
+            // (4.2-5.7 drained); in this kernel C2 went 31.3 -> 30.8 us (NPR_ROWS_PER_LANE: the
+            // per-lane stores).
+            const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
+            const uint64_t f0 = xo + okb;
+            if (nok && f0 + nok <= kp.flow_cap) {
+              const bool mine = (bal >> lane) & 1ull;
+              const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+              const uint64_t p = base + fl[q][7];
+              const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+              u32x4 *stg = reinterpret_cast<u32x4 *>(sh.w[wid].data[0]);
+              if (mine) {
+                const uint32_t k = nok - 1u - rank;  // rank r lands at row flow_cap - 1 - (f0 + r)
+                stg[2 * k] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
+                stg[2 * k + 1] = u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+              }
+              wave_sync();
+              u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
+              if ((uint32_t)lane < 2u * nok) dst[lane] = stg[lane];
+              if ((uint32_t)lane + 64u < 2u * nok) dst[lane + 64] = stg[lane + 64];
+              if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
+#ifdef NPR_ROWS_DRAIN  // (drained rounds measured 31.2 vs 30.8 us undrained at C2)
+              __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
+              wave_sync();  // the slot is rewritten by the next round
+            } else if ((bal >> lane) & 1ull) {
+              const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+              if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
+            }
+#else
             if ((bal >> lane) & 1ull) {
               const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
               if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
             }
+#endif
           }
         }
       }
