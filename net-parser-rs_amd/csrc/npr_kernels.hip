@@ -2426,26 +2426,35 @@ __global__ __launch_bounds__(kBlock) void k_extract_dense(const uint8_t *buf, ui
                                                           const npr_record *recs, uint64_t n,
                                                           uint32_t *flows, uint32_t *flows_v6,
                                                           uint8_t *status) {
-  __shared__ uint32_t rows[kBlock * kRowWords];
-  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  const npr_record rc = load_record(recs, i);
-  FlowWords f{};
-  const uint32_t st = extract_one(buf, len, rc, rows + threadIdx.x * kRowWords, f);
-  const bool ok = st == NPR_FLOW_OK;
-  const bool is6 = ok && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16));
-  uint4 r0, r1, s0, s1;
-  flow_rows(f, rc.offset, ok, is6, r0, r1, s0, s1);
-  if (status) status[i] = (uint8_t)st;
-  if (flows) {
-    uint4 *dst = reinterpret_cast<uint4 *>(flows + i * 8);
-    dst[0] = r0;
-    dst[1] = r1;
+  __shared__ __attribute__((aligned(16))) uint32_t rows[kBlock * kRowWords];
+  static_assert(kBlock * 8 <= kBlock * kRowWords, "the row staging fits the window rows");
+  const uint64_t b0 = (uint64_t)blockIdx.x * kBlock, i = b0 + threadIdx.x;
+  const bool act = i < n;
+  uint4 r0{}, r1{}, s0{}, s1{};
+  if (act) {
+    const npr_record rc = load_record(recs, i);
+    FlowWords f{};
+    const uint32_t st = extract_one(buf, len, rc, rows + threadIdx.x * kRowWords, f);
+    const bool ok = st == NPR_FLOW_OK;
+    const bool is6 = ok && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16));
+    flow_rows(f, rc.offset, ok, is6, r0, r1, s0, s1);
+    if (status) status[i] = (uint8_t)st;
   }
-  if (flows_v6) {
-    uint4 *d6 = reinterpret_cast<uint4 *>(flows_v6 + i * 8);
-    d6[0] = s0;
-    d6[1] = s1;
+  // The block's rows are contiguous: stage them in LDS (the windows are done) and store whole
+  // lines, 16-B chunk c by thread c % kBlock (one 32-B row per lane at a 32-B stride writes at a
+  // fraction of the rate: scripts/microbench/store_pattern.hip)
+  const uint32_t nch = 2u * (uint32_t)(n - b0 < (uint64_t)kBlock ? n - b0 : (uint64_t)kBlock);
+  uint4 *stg = reinterpret_cast<uint4 *>(rows);
+  for (int t = 0; t < 2; ++t) {
+    uint32_t *out = t == 0 ? flows : flows_v6;
+    if (!out) continue;  // (uniform)
+    __syncthreads();
+    stg[2 * threadIdx.x] = t == 0 ? r0 : s0;
+    stg[2 * threadIdx.x + 1] = t == 0 ? r1 : s1;
+    __syncthreads();
+    uint4 *dst = reinterpret_cast<uint4 *>(out + b0 * 8);
+    if (threadIdx.x < nch) dst[threadIdx.x] = stg[threadIdx.x];
+    if (threadIdx.x + kBlock < nch) dst[threadIdx.x + kBlock] = stg[threadIdx.x + kBlock];
   }
 }
 
