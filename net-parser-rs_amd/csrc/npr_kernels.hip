@@ -2687,22 +2687,39 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
   __syncthreads();
   const uint64_t excl = excl_sh;
   if (excl == ~0ull) return;
-  // rows: excl + the Ok flows of this block at higher record indices (later r, higher wave, higher lane)
+  // rows: excl + the Ok flows of this block at higher record indices (later r, higher wave, higher
+  // lane).  Each round's rows are one contiguous block: staged in LDS, stored as whole lines (one
+  // 32-B row per lane at a 32-B stride writes at a fraction of the rate: store_pattern.hip)
+  __shared__ __attribute__((aligned(16))) uint4 cstg[kBlock * 2];
   uint64_t after = excl;
 #pragma unroll
   for (int r = kCvtPer - 1; r >= 0; --r) {
     const bool ok = (okm >> r) & 1u;
     const uint64_t bal = __ballot(ok);
-    uint32_t above = 0;
+    uint32_t above = 0, rc = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / kWave; ++w) above += (uint32_t)w > wave ? wc[r][w] : 0u;
+    for (int w = 0; w < kBlock / kWave; ++w) {
+      above += (uint32_t)w > wave ? wc[r][w] : 0u;
+      rc += wc[r][w];
+    }
+    const uint32_t lr = above + (uint32_t)__builtin_popcountll(bal & ~((2ull << lane) - 1ull));
+    __syncthreads();  // the previous round's chunks are read
     if (ok) {
-      const uint64_t rw = after + above + (uint64_t)__builtin_popcountll(bal & ~((2ull << lane) - 1ull));
+      const bool is6 = (kd[r][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+      cstg[2 * lr] = make_uint4(is6 ? 0u : kd[r][0], kd[r][1], kd[r][2], kd[r][3]);
+      cstg[2 * lr + 1] = make_uint4(kd[r][4], kd[r][5], kd[r][6] | ((uint32_t)(koff[r] & 0xffu) << 24), (uint32_t)(koff[r] >> 8));
+    }
+    __syncthreads();
+    uint4 *blk = reinterpret_cast<uint4 *>(out + after * 8);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t c = threadIdx.x + (uint32_t)h * kBlock;
+      if (c < 2u * rc && after + c / 2u < cap) blk[c] = cstg[c];
+    }
+    if (ok) {
+      const uint64_t rw = after + lr;
       if (rw < cap) {
         const bool is6 = (kd[r][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-        uint4 *dst = reinterpret_cast<uint4 *>(out + rw * 8);
-        dst[0] = make_uint4(is6 ? 0u : kd[r][0], kd[r][1], kd[r][2], kd[r][3]);
-        dst[1] = make_uint4(kd[r][4], kd[r][5], kd[r][6] | ((uint32_t)(koff[r] & 0xffu) << 24), (uint32_t)(koff[r] >> 8));
         if (out_v6 && is6) {  // side rows of IPv6 flows only (as the resident pass: npr.h)
           uint32_t a[8];
           const uint64_t po = koff[r] + 16;  // the 32 address bytes, re-read (the payload lies inside the buffer)
@@ -2715,9 +2732,6 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
         }
       }
     }
-    uint32_t rc = 0;
-#pragma unroll
-    for (int w = 0; w < kBlock / kWave; ++w) rc += wc[r][w];
     after += rc;
   }
 }
