@@ -2200,10 +2200,15 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
               }
               wave_sync();
               u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
+#ifndef NPR_ROWS_WB  // non-temporal (streaming) stores: 30.1 vs 30.6 us at C2 with write-back ones
+              if ((uint32_t)lane < 2u * nok) __builtin_nontemporal_store(stg[lane], dst + lane);
+              if ((uint32_t)lane + 64u < 2u * nok) __builtin_nontemporal_store(stg[lane + 64], dst + lane + 64);
+#else
               if ((uint32_t)lane < 2u * nok) dst[lane] = stg[lane];
               if ((uint32_t)lane + 64u < 2u * nok) dst[lane + 64] = stg[lane + 64];
+#endif
               if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
-#ifdef NPR_ROWS_DRAIN  // (drained rounds measured 31.2 vs 30.8 us undrained at C2)
+#ifdef NPR_ROWS_DRAIN  // (drained rounds measured 31.2 vs 30.8 us undrained at C2, 30.9 vs 30.6 again)
               __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
 #endif
               wave_sync();  // the slot is rewritten by the next round
