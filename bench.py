@@ -318,12 +318,7 @@ def run_sharded(args, dev, local, rank, world):
     return out
 
 
-def main():
-    # the one JSON line goes to the original stdout; everything else written to fd 1 (e.g. the RCCL
-    # version banner of communicator init) goes to stderr
-    out_fd = os.dup(1)
-    os.dup2(2, 1)
-    json_out = os.fdopen(out_fd, "w")
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
@@ -339,11 +334,74 @@ def main():
     ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
     ap.add_argument("--sharded", action="store_true",
                     help="c4 through the multi-GPU step (RCCL exchange + gather) even at N=1")
-    args = ap.parse_args()
+    # the launcher alone, on CPU: every rank joins a gloo group and rank 0 prints the world it saw
+    ap.add_argument("--launch-check", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(rank, world, port, argv):
+    """One spawned rank: the torchrun environment, then the rank's run."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rank_main(parse_args(argv))
+
+
+def spawn_ranks(args, argv):
+    """`python bench.py --gpus N` with no launcher: start N rank processes (one per GPU) before this
+    process touches any GPU, as torch.distributed.run would, and exit with the worst exit code."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's state is inherited
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, argv)) for r in range(args.gpus)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join()
+    codes = [p.exitcode for p in procs]
+    bad = [c for c in codes if c != 0]
+    if bad:
+        print(f"bench.py: rank exit codes {codes}", file=sys.stderr, flush=True)
+        sys.exit(bad[0] if bad[0] and bad[0] > 0 else 1)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return spawn_ranks(args, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:  # never measure another world than the one asked for
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    rank_main(args)
+
+
+def rank_main(args):
+    # the one JSON line goes to the original stdout; everything else written to fd 1 (e.g. the RCCL
+    # version banner of communicator init) goes to stderr
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    json_out = os.fdopen(out_fd, "w")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.launch_check:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        got = [None] * dist.get_world_size()
+        dist.all_gather_object(got, rank)
+        if rank == 0:
+            print(json.dumps({"launch_check": {"world": dist.get_world_size(), "ranks": got}}), file=json_out,
+                  flush=True)
+        dist.destroy_process_group()
+        return
     if args.config is None:
         args.config = "c2" if world == 1 else "c4"
     sharded = world > 1 or args.sharded
@@ -351,12 +409,14 @@ def main():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local), rank=rank, world_size=world)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the communicator has {dist.get_world_size()} ranks")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if sharded:
         if args.config != "c4":
             raise SystemExit("N > 1 runs the sharded C4 workload (--config c4)")
-        out = run_sharded(args, dev, local, rank, world)
+        out = run_sharded(args, dev, local, rank, dist.get_world_size())
     else:
         out = run_single(args, dev, local)
     if rank == 0:

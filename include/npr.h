@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define NPR_ABI_VERSION 3
+#define NPR_ABI_VERSION 4
 
 /* ---- status of an API call ------------------------------------------------------------ */
 typedef enum npr_status {
@@ -132,6 +132,19 @@ typedef enum npr_flow_status {
   NPR_FLOW_L3_IPV6_UDP_REMAINDER = 24,
   NPR_FLOW_STATUS_COUNT = 25
 } npr_flow_status;
+
+/* The payload the reference's error variant carries for each per-record status (npr_flow_details):
+ *   *_INCOMPLETE (nom level, crate::errors::Error::Incomplete{size}) -> the failing primitive's
+ *       Needed::Size (nom 4.2: a be_u16 needs 2, take!(k) needs k; UDP lengths below 8 wrap as the
+ *       reference's usize does, src/layer4/udp.rs:40);
+ *   *_REMAINDER (flow-level Incomplete{size: rem.len()}, src/flow/layer2/ethernet.rs:67-76,
+ *       src/flow/layer3/ipv4.rs:59-70) -> the bytes left after the layer's parse;
+ *   *_FAILURE (map_opt! / map_res!, msg "Error: Code(<input>, MapOpt|MapRes)") -> start | end << 32:
+ *       the frame offsets (from the payload start) of the failing primitive's input and of its
+ *       parser's input end (the frame's end, or the IP payload's for TCP);
+ *   *_CUSTOM ("Expected version 4, was {}") -> the version nibble;
+ *   NPR_FLOW_L2_ETHERTYPE -> the EtherType (LLDP, or an 802.3 length);
+ *   NPR_FLOW_L3_*_PROTOCOL -> the IP protocol id;  NPR_FLOW_OK, NPR_FLOW_L3_ARP -> 0. */
 
 /* VXLAN inner flows (row f3; off the reference's flow path, which never produces a Vxlan flow,
  * quirk Q13): the outer frame's UDP payload parsed as Vxlan::parse (src/layer4/vxlan.rs:31-48),
@@ -374,16 +387,18 @@ npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
 npr_status npr_vxlan_flows(npr_ctx *ctx, const uint8_t *input, size_t len, const npr_record *records, size_t n,
                            uint32_t dst_port, npr_endianness endianness, npr_flow *flows, npr_flow_v6 *flows_v6,
                            uint8_t *status, uint32_t *vni);
+/* Per-record status and error payload (see above) of extract_flow over caller records, synchronous;
+ * status / detail may be NULL.  The Rust crate calls it only for records whose flow failed. */
+npr_status npr_flow_details(npr_ctx *ctx, const uint8_t *input, size_t len, const npr_record *records, size_t n,
+                            uint8_t *status, uint64_t *detail);
+/* Device form of npr_flow_details, asynchronous on `stream`. */
+npr_status npr_dev_flow_details(npr_ctx *ctx, const void *input, uint64_t len, const npr_record *records,
+                                uint64_t n, uint8_t *status, uint64_t *detail, void *stream);
 /* Dense extract_flow over device-resident records (device npr_record array indexing into
  * `input`; payload = input[offset+16 .. offset+16+actual_length]). */
 npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
                                  const npr_record *records, uint64_t n, npr_flow *flows,
                                  npr_flow_v6 *flows_v6, uint8_t *status, void *stream);
-/* flow::convert_records (src/flow/mod.rs:101-123) over device-resident records, asynchronous on
- * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
- * cap are not written; out_v6[i] only when out[i] is IPv6), *n_out (a device word) = the number of
- * Ok flows, or UINT64_MAX when the launch's bounded look-back timed out.  One kernel pass
- * (DESIGN.md §3.4). */
 /* The distinct-flow table (row f4; new, not in the reference): one row per distinct
  * {family, protocol, src ip, dst ip, src port, dst port} of a device flow table (flows[0..n),
  * flows_v6 its IPv6 side rows or NULL for an IPv4-only table), in the order of the input rows that
@@ -391,7 +406,9 @@ npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
  * row), out_v6[k] its side row, counts[k] = the sum of weights[] over its rows (1 per row when
  * weights is NULL; pass a previous call's counts to merge tables, e.g. one per GPU).  Rows past
  * cap are not written; *n_out (a device word) = the number of distinct flows.  Asynchronous on
- * `stream`; any of out_v6 / counts may be NULL. */
+ * `stream`; any of out_v6 / counts may be NULL.  Rows that tie on the first-seen offset (a record
+ * listed twice, merged tables of several captures) resolve to the lowest input row.  At most 2^30
+ * rows per call (NPR_ERR_ARG above). */
 npr_status npr_dev_flow_aggregate(npr_ctx *ctx, const npr_flow *flows, const npr_flow_v6 *flows_v6,
                                   const uint64_t *weights, uint64_t n, npr_flow *out, npr_flow_v6 *out_v6,
                                   uint64_t *counts, uint64_t cap, uint64_t *n_out, void *stream);
@@ -405,6 +422,11 @@ npr_status npr_dev_flow_aggregate(npr_ctx *ctx, const npr_flow *flows, const npr
 npr_status npr_dev_vxlan_flows(npr_ctx *ctx, const void *input, uint64_t len, const npr_record *records,
                                uint64_t n, uint32_t dst_port, npr_endianness endianness, npr_flow *flows,
                                npr_flow_v6 *flows_v6, uint8_t *status, uint32_t *vni, void *stream);
+/* flow::convert_records (src/flow/mod.rs:101-123) over device-resident records, asynchronous on
+ * `stream`: rows 0.. of out / out_v6 (device) = the Ok flows in REVERSE record order (rows past
+ * cap are not written; out_v6[i] only when out[i] is IPv6), *n_out (a device word) = the number of
+ * Ok flows, or UINT64_MAX when the launch's bounded look-back timed out.  One kernel pass
+ * (DESIGN.md §3.4). */
 npr_status npr_dev_convert_records(npr_ctx *ctx, const void *input, uint64_t len,
                                    const npr_record *records, uint64_t n, npr_flow *out,
                                    npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream);

@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -151,6 +152,53 @@ uint64_t tiles_for(uint64_t len, uint64_t start, uint64_t *org_out) {
 }
 
 hipStream_t pick(npr_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+// ---- launch order across contexts ------------------------------------------------------------
+// The look-back kernels (k_parse_resident, the two-pass folds, k_convert_records) have workgroups
+// that wait for lower workgroups of the SAME launch, which is safe only while no other such launch
+// interleaves with it on the device: workgroups are dealt round-robin to the XCDs and each XCD
+// dispatches its share in order, so two launches in flight can each hold the CUs the other's lower
+// workgroups need (two contexts on two streams deadlocked until the bounded waits
+// aborted).  So these launches are serialised per device, process-wide: each waits for an event
+// recorded behind the previous one (whatever context or stream issued it) and records its own.
+// The reference's functions are pure and reentrant (src/errors.rs:13-14: its errors are Send +
+// Sync); with this, any number of host threads with their own contexts may call the C-ABI at once.
+constexpr int kOrderEvents = 8;   // a ring: a wait captures the event's last record when enqueued
+constexpr int kMaxDevices = 64;
+struct DeviceOrder {
+  std::mutex m;
+  hipEvent_t ev[kOrderEvents] = {};
+  int cur = -1;  // the event behind the last ordered launch (-1: none yet)
+};
+DeviceOrder &device_order(int dev) {
+  static DeviceOrder orders[kMaxDevices];
+  return orders[dev & (kMaxDevices - 1)];
+}
+bool launch_order_enabled() {  // (NPR_LAUNCH_ORDER=0: off, for A/B timing of the event cost only)
+  static const bool on = [] {
+    const char *e = getenv("NPR_LAUNCH_ORDER");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+// Run `launch` (enqueues one look-back kernel on s) after every earlier look-back launch on this
+// device; the device's order lock is held from the wait to the record.
+template <class F>
+npr_status ordered_launch(npr_ctx *c, hipStream_t s, F &&launch) {
+  if (!launch_order_enabled()) {
+    HIP_CHECK(c, launch());
+    return NPR_OK;
+  }
+  DeviceOrder &o = device_order(c->device);
+  std::lock_guard<std::mutex> g(o.m);
+  if (o.cur >= 0) HIP_CHECK(c, hipStreamWaitEvent(s, o.ev[o.cur], 0));
+  HIP_CHECK(c, launch());
+  const int k = (o.cur + 1) % kOrderEvents;
+  if (!o.ev[k]) HIP_CHECK(c, hipEventCreateWithFlags(&o.ev[k], hipEventDisableTiming));
+  HIP_CHECK(c, hipEventRecord(o.ev[k], s));
+  o.cur = k;
+  return NPR_OK;
+}
 
 }  // namespace
 
@@ -591,7 +639,7 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
                   (unsigned long long)nb);
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
   }
-  HIP_CHECK(c, npr::launch_parse_extract(p, s));
+  if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_extract(p, s); }))) return st;
   c->sum_ptr[c->sum_next] = o->summary;  // who wrote which summary (chained launches check it)
   c->sum_epoch[c->sum_next] = c->epoch;
   c->sum_next ^= 1u;
@@ -617,17 +665,17 @@ static npr_status convert_launch(npr_ctx *c, const void *input, uint64_t len, co
   npr_status st = ensure(c, c->slots, std::max<uint64_t>(npr::convert_look_words(n), 1) * 8, true);
   if (st) return st;
   if ((st = next_epoch(c, s))) return st;
-  HIP_CHECK(c, npr::launch_convert_records((const uint8_t *)input, len, recs, n, (uint32_t *)out, (uint32_t *)out_v6,
-                                           cap, (uint64_t *)c->slots.p, c->epoch, total,
-                                           kTimeoutTicks, s));
-  return NPR_OK;
+  return ordered_launch(c, s, [&] {
+    return npr::launch_convert_records((const uint8_t *)input, len, recs, n, (uint32_t *)out, (uint32_t *)out_v6, cap,
+                                       (uint64_t *)c->slots.p, c->epoch, total, kTimeoutTicks, s);
+  });
 }
 
 npr_status npr_dev_flow_aggregate(npr_ctx *c, const npr_flow *flows, const npr_flow_v6 *flows_v6,
                                   const uint64_t *weights, uint64_t n, npr_flow *out, npr_flow_v6 *out_v6,
                                   uint64_t *counts, uint64_t cap, uint64_t *n_out, void *stream) {
   if (!c || (!flows && n) || !n_out || (!out && cap)) return fail(c, NPR_ERR_ARG, "null argument");
-  if (n > 0xffffffffull) return fail(c, NPR_ERR_ARG, "at most 2^32 - 1 flow rows per call");
+  if (n > npr::kMaxAggRows) return fail(c, NPR_ERR_ARG, "at most 2^30 flow rows per call");
   HIP_CHECK(c, hipSetDevice(c->device));
   npr_status st = ensure(c, c->agg, npr::flow_table_bytes(n));
   if (st) return st;
@@ -644,6 +692,14 @@ npr_status npr_dev_vxlan_flows(npr_ctx *c, const void *input, uint64_t len, cons
   HIP_CHECK(c, hipSetDevice(c->device));
   HIP_CHECK(c, npr::launch_vxlan_flows((const uint8_t *)input, len, recs, n, dst_port, e == NPR_BIG, (uint32_t *)flows,
                                        (uint32_t *)flows_v6, status, vni, pick(c, stream)));
+  return NPR_OK;
+}
+
+npr_status npr_dev_flow_details(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
+                                uint8_t *status, uint64_t *detail, void *stream) {
+  if (!c || (!input && len) || (!recs && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  HIP_CHECK(c, npr::launch_flow_detail((const uint8_t *)input, len, recs, n, status, detail, pick(c, stream)));
   return NPR_OK;
 }
 
@@ -1149,6 +1205,25 @@ npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const np
   if (flows_v6)
     HIP_CHECK(c, hipMemcpyAsync(flows_v6, c->flows_v6.p, n * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));
   if (status) HIP_CHECK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(c, hipStreamSynchronize(c->stream));
+  return NPR_OK;
+}
+
+npr_status npr_flow_details(npr_ctx *c, const uint8_t *in, size_t len, const npr_record *records, size_t n,
+                            uint8_t *status, uint64_t *detail) {
+  if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = stage_input(c, in, len);
+  if (st) return st;
+  if (n == 0) return NPR_OK;
+  if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
+  if ((st = ensure(c, c->status, n))) return st;
+  if ((st = ensure(c, c->flows2, n * sizeof(uint64_t)))) return st;  // the details
+  HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
+  HIP_CHECK(c, npr::launch_flow_detail((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n,
+                                       (uint8_t *)c->status.p, (uint64_t *)c->flows2.p, c->stream));
+  if (status) HIP_CHECK(c, hipMemcpyAsync(status, c->status.p, n, hipMemcpyDeviceToHost, c->stream));
+  if (detail) HIP_CHECK(c, hipMemcpyAsync(detail, c->flows2.p, n * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(c, hipStreamSynchronize(c->stream));
   return NPR_OK;
 }

@@ -137,20 +137,32 @@ __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const 
   }
 }
 
-// is row i its slot's first-seen row?  (record offsets are unique per row)
-__device__ __forceinline__ bool is_first(const uint32_t *flows, const uint32_t *slot_of_row, const uint64_t *slot_first,
-                                         uint64_t i) {
-  return row_offset(flows + i * 8) == slot_first[slot_of_row[i]];
+// Ties: several rows of one slot may carry the slot's first-seen offset (a record listed twice,
+// or tables of several captures merged: every capture's first record sits at offset 24).  The
+// slot's first-seen ROW is the lowest row index among them (the input order the output keeps):
+// one atomic min per tied row into the slot's word, which the insert no longer needs (its claims
+// are done), reset to ~0 in between.
+__global__ __launch_bounds__(kB) void k_agg_tie(const uint32_t *flows, const uint32_t *slot_of_row,
+                                                const uint64_t *slot_first, uint64_t n, uint64_t *slot_row) {
+  const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t pos = slot_of_row[i];
+  if (row_offset(flows + i * 8) == slot_first[pos]) atomicMin((unsigned long long *)(slot_row + pos), (unsigned long long)i);
 }
 
-__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *flows, const uint32_t *slot_of_row,
-                                                  const uint64_t *slot_first, uint64_t n, uint32_t *block_counts) {
+// is row i its slot's first-seen row?
+__device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t i) {
+  return slot_row[slot_of_row[i]] == i;
+}
+
+__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t n,
+                                                  uint32_t *block_counts) {
   __shared__ uint32_t sc[kB / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kAggItems;
   uint32_t c = 0;
   for (int k = 0; k < kAggItems / kB; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    c += (i < n && is_first(flows, slot_of_row, slot_first, i)) ? 1u : 0u;
+    c += (i < n && is_first(slot_of_row, slot_row, i)) ? 1u : 0u;
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63u) == 0) sc[threadIdx.x >> 6] = c;
@@ -181,7 +193,7 @@ __global__ __launch_bounds__(kB) void k_agg_scan(uint32_t *counts, uint64_t nb, 
 }
 
 __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const uint32_t *flows_v6,
-                                                    const uint32_t *slot_of_row, const uint64_t *slot_first,
+                                                    const uint32_t *slot_of_row, const uint64_t *slot_row,
                                                     const uint64_t *slot_count, uint64_t n, const uint32_t *offsets,
                                                     uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap) {
   __shared__ uint32_t sc[kAggItems / kB][kB / 64];
@@ -191,7 +203,7 @@ __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const
 #pragma unroll
   for (int k = 0; k < kAggItems / kB; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    first[k] = i < n && is_first(flows, slot_of_row, slot_first, i);
+    first[k] = i < n && is_first(slot_of_row, slot_row, i);
     const uint64_t bal = __ballot(first[k]);
     if (lane == 0) sc[k][wave] = (uint32_t)__builtin_popcountll(bal);
   }
@@ -228,7 +240,7 @@ __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const
 
 }  // namespace
 
-uint64_t flow_table_slots(uint64_t n) {  // (slot indices must fit the LDS table's u32 keys)
+uint64_t flow_table_slots(uint64_t n) {  // n <= kMaxAggRows: S <= 2^31, so a slot index < 2^31 never equals ~0
   uint64_t s = 1024;
   while (s < 2 * n) s <<= 1;
   return s;
@@ -242,7 +254,7 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
                                  void *work, uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap,
                                  uint64_t *total, hipStream_t s) {
   if (n == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
-  if (n > 0xffffffffull) return hipErrorInvalidValue;  // row indices are 32-bit in the slot words
+  if (n > kMaxAggRows) return hipErrorInvalidValue;  // slot indices are 32-bit, ~0 marks an empty LDS entry
   const uint64_t S = flow_table_slots(n), nb = (n + kAggItems - 1) / kAggItems;
   uint64_t *slot_word = (uint64_t *)work, *slot_first = slot_word + S, *slot_count = slot_first + S;
   uint32_t *slot_of_row = (uint32_t *)(slot_count + S), *block = slot_of_row + n;
@@ -252,9 +264,13 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
   if ((e = hipMemsetAsync(slot_count, 0, S * 8, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_agg_insert, dim3((uint32_t)((n + kInsRows - 1) / kInsRows)), dim3(kB), 0, s, flows, flows_v6, weights, n,
                      slot_word, slot_first, slot_count, slot_of_row, S - 1);
-  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, flows, slot_of_row, slot_first, n, block);
+  uint64_t *slot_row = slot_word;  // the claims are done: the word now holds the first-seen row
+  if ((e = hipMemsetAsync(slot_row, 0xff, S * 8, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_agg_tie, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, slot_of_row, slot_first, n,
+                     slot_row);
+  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, n, block);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(kB), 0, s, block, nb, total);
-  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, slot_first,
+  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, slot_row,
                      slot_count, n, block, out, out_v6, counts, cap);
   return hipGetLastError();
 }

@@ -143,6 +143,9 @@ constexpr uint32_t kPipeGroupTiles = 15;  // tiles per group slot of the pipelin
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);
+// the payload of each record's extract_flow error (status and detail may each be NULL)
+hipError_t launch_flow_detail(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint8_t *status,
+                              uint64_t *detail, hipStream_t s);
 // row f3: VXLAN inner flows (dense, row i for record i; any output may be NULL)
 hipError_t launch_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint32_t dst_port,
                               bool big, uint32_t *flows, uint32_t *flows_v6, uint8_t *status, uint32_t *vni,
@@ -153,6 +156,7 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
                                  void *work, uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap,
                                  uint64_t *total, hipStream_t s);
 uint64_t flow_table_bytes(uint64_t n);
+constexpr uint64_t kMaxAggRows = 1ull << 30;  // rows per call: S = 2^31 slots, 32-bit slot indices
 // convert_records in one pass (k_convert_records): rows 0.. = Ok flows in reverse record order,
 // *total = all Ok flows (rows past cap are not written; ~0 when a bounded wait timed out).
 // look: convert_look_words(n) granules whose tags are not `epoch` at launch.

@@ -192,7 +192,8 @@ class PcapRecord:
         flows, v6, status = flow._extract(self._buf, [self])
         st = int(status[0])
         if st != 0:
-            raise flow.FlowError(st)
+            _, det = flow._details(self._buf, [self])
+            raise flow.FlowError(st, det[0])
         return flow.Flow._from_row(flows[0], v6[0])
 
 

@@ -106,6 +106,7 @@ EXPORTED = [
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
+    "npr_flow_details", "npr_dev_flow_details",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -162,6 +163,8 @@ _SIGNATURES = {
                                               _vp, _vp]),
     "npr_vxlan_flows": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, ctypes.c_uint32,
                                        ctypes.c_int, _vp, _vp, _vp, _vp]),
+    "npr_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
+    "npr_dev_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
 }
 
 _lib = None

@@ -70,13 +70,39 @@ class Flow:
                     "Udp" if kind & _abi.KIND_UDP else "Tcp", row["vlan"], record_offset=off)
 
 
-class FlowError(Exception):
-    """flow::errors::Error (src/flow/errors.rs:5-19); `.code` is the npr_flow_status leaf."""
+# npr_flow_status leaves whose variant carries a size (include/npr.h npr_flow_details): nom-level
+# Incomplete (Needed::Size) and the flow-level remainders (rem.len())
+_SIZED = {1, 4, 7, 10, 17, 19, 20, 22} | {11, 12, 13, 23, 24}
 
-    def __init__(self, code):
+
+class FlowError(Exception):
+    """flow::errors::Error (src/flow/errors.rs:5-19); `.code` is the npr_flow_status leaf, `.detail`
+    the payload its variant carries (npr_flow_details: a size, an offset, a version, an EtherType
+    or a protocol id; None when not computed) and `.size` the `size` field of the sized variants."""
+
+    def __init__(self, code, detail=None):
         self.code = int(code)
+        self.detail = None if detail is None else int(detail)
         self.name = _abi.FLOW_STATUS_NAME.get(self.code, f"UNKNOWN_{code}")
-        super().__init__(self.name)
+        super().__init__(self.name if self.detail is None else f"{self.name}({self.detail})")
+
+    @property
+    def size(self):
+        return self.detail if self.code in _SIZED else None
+
+
+def _details(buf, records):
+    """(status, detail) of extract_flow over records indexing into `buf` (npr_flow_details)."""
+    from . import context
+    ctx = context()
+    a = np.ascontiguousarray(buf, dtype=np.uint8).reshape(-1)
+    t = _table(records)
+    n = len(t)
+    status = np.zeros(max(n, 1), dtype=np.uint8)
+    detail = np.zeros(max(n, 1), dtype=np.uint64)
+    ctx.check(ctx.lib.npr_flow_details(ctx.handle, a.ctypes.data if a.size else None, a.size, t.ctypes.data, n,
+                                       status.ctypes.data, detail.ctypes.data))
+    return status[:n], detail[:n]
 
 
 def _table(records):

@@ -177,7 +177,8 @@ def gather_flow_tables(flows, flows_v6, metas: List[ShardResult], live, group=No
     place in the merged table (no padding, no concatenation pass): rank r's rows land at
     merged_positions()[r].  `flows` / `flows_v6` are this rank's n_flows rows as uint8 tensors
     (n_flows * 32 bytes) on the backend's device: CUDA tensors over RCCL (xGMI), CPU tensors over
-    gloo; flows_v6 may be None (then no side table is gathered).  Returns (merged, merged_v6)
+    gloo; flows_v6 may be None (then no side table is gathered; every rank must pass a side table,
+    possibly empty, or every rank None: the transfers are matched pairwise).  Returns (merged, merged_v6)
     uint8 tensors on dst, (None, None) elsewhere."""
     import torch
     import torch.distributed as dist
@@ -217,16 +218,20 @@ def gather_flow_tables(flows, flows_v6, metas: List[ShardResult], live, group=No
 def gather_flows(mine: ShardResult, metas: List[ShardResult], live, group=None, dst=0):
     """gather_flow_tables over this rank's rows (numpy or tensors); on dst returns the merged
     (flows, flows_v6) as numpy record arrays (flows_v6 None when the ranks hold none)."""
+    import torch
     import torch.distributed as dist
     rank = dist.get_rank(group)
     ok = live[rank] and mine.n_flows
-    fl = _as_bytes_tensor(mine.flows) if ok else None
-    v6 = _as_bytes_tensor(mine.flows_v6) if ok else None
-    if fl is None:
-        import torch
-        fl = torch.zeros(0, dtype=torch.uint8)
-    # every rank must agree on whether a side table moves: gather it when this rank has one
-    out, out6 = gather_flow_tables(fl, v6 if mine.flows_v6 is not None else None, metas, live, group=group, dst=dst)
+    empty = torch.zeros(0, dtype=torch.uint8)
+    fl = _as_bytes_tensor(mine.flows) if ok else empty
+    # every rank must agree on whether a side table moves (a rank with no rows still takes part:
+    # the root posts one receive per contributing rank's side rows): side rows move only when every
+    # rank holds a side table, decided by one all-reduce of the flag
+    flag = torch.tensor([1 if mine.flows_v6 is not None else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    with_v6 = bool(flag.item())
+    v6 = (_as_bytes_tensor(mine.flows_v6) if ok else empty) if with_v6 else None
+    out, out6 = gather_flow_tables(fl, v6, metas, live, group=group, dst=dst)
     if out is None:
         return None
     f = out.cpu().numpy().view(_abi.FLOW_DTYPE)
@@ -336,6 +341,20 @@ class DeviceShardedParse:
         self.ws.launch_shard(self.buf, self.base, start, hi, endianness=self.e, speculative=speculative,
                              usec_magic=self.usec, ts_ref=self.ts_ref, chunk_bytes=self.chunk, nbytes=self.nbytes)
 
+    def _empty_summary(self, e):
+        """The summary of a shard no record starts in (the exact entry e is at or past its stop):
+        {entry = consumed = e, no records, no flows}, what exact_result() builds on the host path.
+        Written in place of a launch, so this rank keeps taking part in the exchange."""
+        import torch
+        s = np.zeros(1, dtype=_abi.SUMMARY_DTYPE)
+        s["entry"], s["consumed"], s["n_records"], s["n_flows"] = e, e, 0, 0
+        s["flags"], s["epoch"] = 0, 1  # epoch != 0: a completed parse (_metas)
+        if torch.cuda.is_available() and self.ws.summary.is_cuda:
+            torch.cuda.current_stream().synchronize()  # no launch of this step still writes the summary
+        raw = torch.from_numpy(s.view(np.uint8).copy())
+        self.ws.summary.zero_()
+        self.ws.summary[: raw.numel()].copy_(raw.to(self.ws.summary.device))
+
     def _metas(self, host_bytes):
         g = host_bytes.numpy().reshape(self.world, -1)[:, :40].copy().view(_abi.SUMMARY_DTYPE).reshape(-1)
         if (g["epoch"] == 0).any() or (g["flags"] != 0).any():
@@ -423,9 +442,10 @@ class DeviceShardedParse:
             if bad is None:
                 break
             if bad == self.rank:
-                if e >= hi:
-                    raise HaloError(f"rank {self.rank}: a record spans the whole shard; not supported by the device step")
-                self._launch(e, False)
+                if e >= hi:  # one record spans this whole shard: no record starts here (replay's rule)
+                    self._empty_summary(e)
+                else:
+                    self._launch(e, False)
             else:  # keep the stream order: an empty launch is not needed, the others just re-gather
                 pass
             rounds += 1

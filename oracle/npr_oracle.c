@@ -9,9 +9,18 @@
 
 #include <string.h>
 
+/* The error payload of the last failing step (npr.h "npr_flow_details"): g_need = the failing
+ * primitive's Needed::Size (nom 4.2 primitives report their full size: be_u16 -> 2, take!(k) -> k),
+ * g_fail = the input position (in the failing parser's own input) of a map_opt! / map_res! failure.
+ * Thread-local: the bench leg runs the parsers on several threads. */
+static _Thread_local uint64_t g_need, g_fail;
+
 #define NEED(k)                                                                                    \
   do {                                                                                             \
-    if ((size_t)(n - pos) < (size_t)(k)) return OR_INCOMPLETE;                                     \
+    if ((size_t)(n - pos) < (size_t)(k)) {                                                         \
+      g_need = (uint64_t)(size_t)(k);                                                              \
+      return OR_INCOMPLETE;                                                                        \
+    }                                                                                              \
   } while (0)
 
 static uint16_t rd_be16(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
@@ -121,7 +130,7 @@ int or_eth_parse(const uint8_t *in, size_t n, or_eth *v) {
     NEED(2);
     uint16_t t = rd_be16(in + pos); pos += 2;   /* map_opt!(be_u16, EthernetTypeId::new) :170 */
     int cls = eth_type_class(t);
-    if (cls == 0) return OR_FAILURE;
+    if (cls == 0) { g_fail = pos - 2; return OR_FAILURE; } /* map_opt!'s input: the type field */
     if (cls == 1) {
       NEED(2);
       uint16_t tci = rd_be16(in + pos); pos += 2; /* total: be_u16 :176 */
@@ -166,7 +175,7 @@ int or_ipv4_parse(const uint8_t *in, size_t n, or_ip *v) {
   NEED(1); pos += 1;                                          /* ttl :118 */
   NEED(1);
   uint8_t protocol = in[pos]; pos += 1;                       /* map_opt! :119 */
-  if (!ip_proto_known(protocol)) return OR_FAILURE;
+  if (!ip_proto_known(protocol)) { g_fail = pos - 1; return OR_FAILURE; }
   NEED(2); pos += 2;                                          /* checksum :120 */
   NEED(4); v->src = in + pos; pos += 4;                       /* src_ip :121 */
   NEED(4); v->dst = in + pos; pos += 4;                       /* dst_ip :122 */
@@ -190,10 +199,10 @@ int or_ipv6_parse(const uint8_t *in, size_t n, or_ip *v) {
   NEED(3); pos += 3;                                          /* _f: take!(3) :61 */
   NEED(2); uint16_t payload_length = rd_be16(in + pos); pos += 2; /* p: be_u16 :62 */
   NEED(1); uint8_t nh = in[pos]; pos += 1;                    /* h: map_opt! :63 */
-  if (!ip_proto_known(nh)) return OR_FAILURE;
+  if (!ip_proto_known(nh)) { g_fail = pos - 1; return OR_FAILURE; }
   while (ip_proto_has_next(nh)) {                             /* parse_next_header :34-37 */
     NEED(1); nh = in[pos]; pos += 1;                          /* map_opt!(be_u8, ..) :35 */
-    if (!ip_proto_known(nh)) return OR_FAILURE;
+    if (!ip_proto_known(nh)) { g_fail = pos - 1; return OR_FAILURE; }
   }
   NEED(1); pos += 1;                                          /* _h: take!(1) hop limit :41 */
   NEED(16); v->src = in + pos; pos += 16;                     /* :42 */
@@ -230,7 +239,7 @@ int or_tcp_parse(const uint8_t *in, size_t n, or_l4 *v) {
   NEED(2);
   uint16_t hv = rd_be16(in + pos); pos += 2;                  /* map_res!(be_u16, ..) :68 */
   size_t hl = or_tcp_extract_length(hv);                      /* extract_length :54-57 */
-  if (!(hl >= 20 && hl <= 60)) return OR_FAILURE;             /* :71-82 */
+  if (!(hl >= 20 && hl <= 60)) { g_fail = pos - 2; return OR_FAILURE; } /* map_res! :71-82 */
   NEED(2); pos += 2; NEED(2); pos += 2; NEED(2); pos += 2;    /* window/check/urgent :84-86 */
   NEED(hl - 20); pos += hl - 20;                              /* options :87 */
   v->header_length = hl;
@@ -261,11 +270,14 @@ static void put_offset(npr_flow *f, uint64_t off) {
 /* ---- src/flow/mod.rs:23-41 + src/flow/layer{2,3,4}/ (per-layer impls) ---------------------------------- */
 /* l4 / l4n (optional): the L4 header's start and length (the IP payload) of an Ok flow */
 static int extract_flow_l4(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f, npr_flow_v6 *v6,
-                           const uint8_t **l4_out, size_t *l4n_out) {
+                           const uint8_t **l4_out, size_t *l4n_out, uint64_t *det) {
+  uint64_t dummy;
+  if (!det) det = &dummy;
+  *det = 0;
   or_eth e;
   int rc = or_eth_parse(p, n, &e); /* Ethernet::parse, mod.rs:28-31 */
-  if (rc == OR_INCOMPLETE) return NPR_FLOW_ETH_INCOMPLETE;
-  if (rc != OR_OK) return NPR_FLOW_ETH_FAILURE;
+  if (rc == OR_INCOMPLETE) { *det = g_need; return NPR_FLOW_ETH_INCOMPLETE; }
+  if (rc != OR_OK) { *det = g_fail | ((uint64_t)n << 32); return NPR_FLOW_ETH_FAILURE; }
   /* rem is always empty (payload = rest), so mod.rs:33-40 never fails. */
   const uint8_t *l3 = p + e.payload_off;
   size_t l3n = n - e.payload_off;
@@ -274,27 +286,28 @@ static int extract_flow_l4(const uint8_t *p, size_t n, uint64_t record_offset, n
   switch (e.ether_type) { /* flow/layer2/ethernet.rs:55-131 */
   case 0x0800:
     rc = or_ipv4_parse(l3, l3n, &ip);
-    if (rc == OR_INCOMPLETE) return NPR_FLOW_L2_IPV4_INCOMPLETE;
-    if (rc == OR_FAILURE) return NPR_FLOW_L2_IPV4_FAILURE;
-    if (rc == OR_CUSTOM) return NPR_FLOW_L2_IPV4_CUSTOM;
-    if (ip.rem != 0) return NPR_FLOW_L2_IPV4_REMAINDER; /* :67-76 */
+    if (rc == OR_INCOMPLETE) { *det = g_need; return NPR_FLOW_L2_IPV4_INCOMPLETE; }
+    if (rc == OR_FAILURE) { *det = (e.payload_off + g_fail) | ((uint64_t)n << 32); return NPR_FLOW_L2_IPV4_FAILURE; }
+    if (rc == OR_CUSTOM) { *det = l3[0] >> 4; return NPR_FLOW_L2_IPV4_CUSTOM; }
+    if (ip.rem != 0) { *det = ip.rem; return NPR_FLOW_L2_IPV4_REMAINDER; } /* :67-76 */
     v6flag = 0;
     break;
   case 0x86dd:
     rc = or_ipv6_parse(l3, l3n, &ip);
-    if (rc == OR_INCOMPLETE) return NPR_FLOW_L2_IPV6_INCOMPLETE;
-    if (rc == OR_FAILURE) return NPR_FLOW_L2_IPV6_FAILURE;
-    if (rc == OR_CUSTOM) return NPR_FLOW_L2_IPV6_CUSTOM;
-    if (ip.rem != 0) return NPR_FLOW_L2_IPV6_REMAINDER; /* :91-100 */
+    if (rc == OR_INCOMPLETE) { *det = g_need; return NPR_FLOW_L2_IPV6_INCOMPLETE; }
+    if (rc == OR_FAILURE) { *det = (e.payload_off + g_fail) | ((uint64_t)n << 32); return NPR_FLOW_L2_IPV6_FAILURE; }
+    if (rc == OR_CUSTOM) { *det = l3[0] >> 4; return NPR_FLOW_L2_IPV6_CUSTOM; }
+    if (ip.rem != 0) { *det = ip.rem; return NPR_FLOW_L2_IPV6_REMAINDER; } /* :91-100 */
     v6flag = 1;
     break;
   case 0x0806: {
     or_arp a;
-    if (or_arp_parse(l3, l3n, &a) != OR_OK) return NPR_FLOW_L2_ARP_INCOMPLETE; /* :104-111 */
-    if (a.rem != 0) return NPR_FLOW_L2_ARP_REMAINDER;                           /* :112-122 */
+    if (or_arp_parse(l3, l3n, &a) != OR_OK) { *det = g_need; return NPR_FLOW_L2_ARP_INCOMPLETE; } /* :104-111 */
+    if (a.rem != 0) { *det = a.rem; return NPR_FLOW_L2_ARP_REMAINDER; }                           /* :112-122 */
     return NPR_FLOW_L3_ARP;                                               /* layer3/arp.rs:24-26 */
   }
   default:
+    *det = e.ether_type;
     return NPR_FLOW_L2_ETHERTYPE; /* LLDP / PayloadLength :125-130 */
   }
   /* flow/layer3/ipv4.rs:49-101 and flow/layer3/ipv6.rs:49-100 */
@@ -304,15 +317,19 @@ static int extract_flow_l4(const uint8_t *p, size_t n, uint64_t record_offset, n
   int udp;
   if (ip.protocol == 6) {
     rc = or_tcp_parse(l4, l4n, &t);
-    if (rc == OR_INCOMPLETE) return v6flag ? NPR_FLOW_L3_IPV6_TCP_INCOMPLETE : NPR_FLOW_L3_IPV4_TCP_INCOMPLETE;
-    if (rc != OR_OK) return v6flag ? NPR_FLOW_L3_IPV6_TCP_FAILURE : NPR_FLOW_L3_IPV4_TCP_FAILURE;
+    if (rc == OR_INCOMPLETE) { *det = g_need; return v6flag ? NPR_FLOW_L3_IPV6_TCP_INCOMPLETE : NPR_FLOW_L3_IPV4_TCP_INCOMPLETE; }
+    if (rc != OR_OK) {
+      *det = ((uint64_t)(l4 - p) + g_fail) | ((uint64_t)(l4 - p + l4n) << 32); /* the TCP input is the IP payload */
+      return v6flag ? NPR_FLOW_L3_IPV6_TCP_FAILURE : NPR_FLOW_L3_IPV4_TCP_FAILURE;
+    }
     udp = 0;
   } else if (ip.protocol == 17) {
     rc = or_udp_parse(l4, l4n, &t);
-    if (rc != OR_OK) return v6flag ? NPR_FLOW_L3_IPV6_UDP_INCOMPLETE : NPR_FLOW_L3_IPV4_UDP_INCOMPLETE;
-    if (t.rem != 0) return v6flag ? NPR_FLOW_L3_IPV6_UDP_REMAINDER : NPR_FLOW_L3_IPV4_UDP_REMAINDER;
+    if (rc != OR_OK) { *det = g_need; return v6flag ? NPR_FLOW_L3_IPV6_UDP_INCOMPLETE : NPR_FLOW_L3_IPV4_UDP_INCOMPLETE; }
+    if (t.rem != 0) { *det = t.rem; return v6flag ? NPR_FLOW_L3_IPV6_UDP_REMAINDER : NPR_FLOW_L3_IPV4_UDP_REMAINDER; }
     udp = 1;
   } else {
+    *det = ip.protocol;
     return v6flag ? NPR_FLOW_L3_IPV6_PROTOCOL : NPR_FLOW_L3_IPV4_PROTOCOL;
   }
   /* Flow::new (flow/mod.rs:64-86) */
@@ -337,7 +354,7 @@ static int extract_flow_l4(const uint8_t *p, size_t n, uint64_t record_offset, n
 }
 
 int or_extract_flow(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f, npr_flow_v6 *v6) {
-  return extract_flow_l4(p, n, record_offset, f, v6, NULL, NULL);
+  return extract_flow_l4(p, n, record_offset, f, v6, NULL, NULL, NULL);
 }
 
 /* ---- row f3: src/layer4/vxlan.rs:31-48 (Vxlan::parse) + src/flow/layer4/vxlan.rs:32-50 ----- */
@@ -359,7 +376,7 @@ int or_vxlan_flow(const uint8_t *p, size_t n, uint64_t record_offset, uint32_t d
   const uint8_t *l4 = NULL;
   size_t l4n = 0;
   *vni = 0;
-  int st = extract_flow_l4(p, n, record_offset, &outer, NULL, &l4, &l4n);
+  int st = extract_flow_l4(p, n, record_offset, &outer, NULL, &l4, &l4n, NULL);
   if (st != NPR_FLOW_OK) return st;
   if (!(outer.kind & NPR_FLOW_KIND_UDP)) return NPR_VXLAN_NOT_UDP;
   if (dst_port && outer.dst_port != dst_port) return NPR_VXLAN_PORT;
@@ -419,6 +436,21 @@ void or_extract_flows(const uint8_t *buf, size_t len, const npr_record *recs, si
     if (flows) flows[i] = f;
     if (flows_v6) flows_v6[i] = v6;
     if (status) status[i] = (uint8_t)st;
+  }
+}
+
+/* The error payload of each record's extract_flow (npr.h npr_flow_details). */
+void or_flow_details(const uint8_t *buf, size_t len, const npr_record *recs, size_t n, uint8_t *status,
+                     uint64_t *detail) {
+  for (size_t i = 0; i < n; ++i) {
+    npr_flow f;
+    npr_flow_v6 v6;
+    uint64_t d = 0;
+    const size_t off = (size_t)recs[i].offset + 16, plen = recs[i].actual_length;
+    int st = -1;
+    if (!(off > len || len - off < plen)) st = extract_flow_l4(buf + off, plen, recs[i].offset, &f, &v6, NULL, NULL, &d);
+    if (status) status[i] = (uint8_t)st;
+    if (detail) detail[i] = d;
   }
 }
 

@@ -53,6 +53,10 @@ size_t or_convert_records(const uint8_t *buf, size_t len, const npr_record *recs
 void or_extract_flows(const uint8_t *buf, size_t len, const npr_record *recs, size_t n,
                       npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status);
 
+/* Per-record status + the payload its error variant carries (include/npr.h npr_flow_details). */
+void or_flow_details(const uint8_t *buf, size_t len, const npr_record *recs, size_t n, uint8_t *status,
+                     uint64_t *detail);
+
 /* row f3: Vxlan::parse (src/layer4/vxlan.rs:31-48) and the VXLAN inner flow */
 typedef struct or_vxlan {
   uint16_t flags, group_policy_id;

@@ -1,4 +1,4 @@
-//! `extern "C"` view of include/npr.h (ABI 3): the entry points this crate binds, with the
+//! `extern "C"` view of include/npr.h (ABI 4): the entry points this crate binds, with the
 //! reference functions they replace.
 #![allow(non_camel_case_types)]
 
@@ -12,7 +12,7 @@ pub const NPR_CUSTOM: npr_status = 3; // Error::Custom (src/errors.rs:9)
 pub const NPR_ERR_CAPACITY: npr_status = -3;
 pub const NPR_LITTLE: c_int = 0;
 pub const NPR_BIG: c_int = 1;
-pub const NPR_ABI_VERSION: c_int = 3;
+pub const NPR_ABI_VERSION: c_int = 4;
 pub const NPR_FLOW_KIND_IPV6: u8 = 0x1;
 pub const NPR_FLOW_KIND_UDP: u8 = 0x2;
 
@@ -74,6 +74,23 @@ pub struct npr_flow_v6 {
 }
 
 extern "C" {
+    /// GlobalHeader::parse (src/global_header.rs:40-70): 24 bytes, host side
+    pub fn npr_global_header_parse(
+        input: *const u8,
+        len: usize,
+        out: *mut npr_global_header,
+        consumed: *mut usize,
+    ) -> npr_status;
+
+    /// PcapRecord::parse (src/record.rs:102-121): one 16-byte header + its payload, host side
+    pub fn npr_record_parse(
+        input: *const u8,
+        len: usize,
+        endianness: c_int,
+        out: *mut npr_record,
+        consumed: *mut usize,
+    ) -> npr_status;
+
     pub fn npr_abi_version() -> c_int;
     pub fn npr_version() -> *const c_char;
     pub fn npr_ctx_create(device: c_int, out: *mut *mut npr_ctx) -> npr_status;
@@ -146,6 +163,17 @@ extern "C" {
         flows_v6: *mut npr_flow_v6,
         status: *mut u8,
         vni: *mut u32,
+    ) -> npr_status;
+
+    /// The payload each record's extract_flow error variant carries (include/npr.h npr_flow_details)
+    pub fn npr_flow_details(
+        ctx: *mut npr_ctx,
+        input: *const u8,
+        len: usize,
+        records: *const npr_record,
+        n: usize,
+        status: *mut u8,
+        detail: *mut u64,
     ) -> npr_status;
 
     pub fn npr_host_alloc(ctx: *mut npr_ctx, bytes: usize, out: *mut *mut c_void) -> npr_status;

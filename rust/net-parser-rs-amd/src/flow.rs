@@ -1,12 +1,13 @@
-//! Flow extraction on the device (src/flow/mod.rs): the FlowExtraction trait, convert_records,
-//! and a fused parse + convert_records.  Flow, Device, info and the error tree are the
-//! reference's own types.
+//! Flow extraction on the device (src/flow/mod.rs): the FlowExtraction trait, convert_records, and
+//! a fused parse + convert_records.  Flow, Device, info and the error tree are this crate's
+//! restatements of the reference's types (types.rs).
 //!
-//! A flow error is rebuilt from the device's per-record status code, one code per leaf of the
-//! reference's error tree (include/npr.h npr_flow_status).  The variant path is exact; the
-//! `size` / `msg` payloads inside it are not computed on the device (`size: None` / `0`,
-//! `msg: ""`), which SURVEY.md §8 a16 leaves out of scope.
-pub use net_parser_rs::flow::{device, errors, info, layer2, layer3, layer4, Flow};
+//! A flow error is rebuilt from the device's per-record status code (one code per leaf of the
+//! reference's error tree, include/npr.h npr_flow_status) and the payload its variant carries
+//! (npr_flow_details: nom's Needed sizes, the bytes a layer left over, the failing primitive's
+//! input, the version, EtherType or protocol id), so `Debug`, `Display` and the `size` fields
+//! compare equal to the reference's.
+pub use crate::types::flow_types::{device, errors, info, layer2, layer3, layer4};
 
 use crate::common::MacAddress;
 use crate::ffi;
@@ -17,8 +18,42 @@ use std::borrow::Cow;
 use std::net::{IpAddr, Ipv4Addr, Ipv6Addr};
 
 ///
+/// Flow that was built from a record moved (src/flow/mod.rs:50-96)
+///
+#[derive(Clone, Copy, Debug, Default, PartialEq, Eq, Hash)]
+pub struct Flow {
+    pub source: Device,
+    pub destination: Device,
+    pub layer2: info::layer2::Id,
+    pub layer3: info::layer3::Id,
+    pub layer4: info::layer4::Id,
+    pub vlan: crate::common::Vlan,
+}
+
+impl Flow {
+    pub fn new(l2: info::layer2::Info, l3: info::layer3::Info, l4: info::layer4::Info) -> Flow {
+        Flow {
+            source: Device { mac: l2.src_mac, ip: l3.src_ip, port: l4.src_port },
+            destination: Device { mac: l2.dst_mac, ip: l3.dst_ip, port: l4.dst_port },
+            layer2: l2.id,
+            layer3: l3.id,
+            layer4: l4.id,
+            vlan: l2.vlan,
+        }
+    }
+}
+
+impl std::fmt::Display for Flow {
+    fn fmt(&self, f: &mut std::fmt::Formatter) -> std::fmt::Result {
+        write!(f, "Source=[{}]   Destination=[{}]   Vlan={}", self.source, self.destination, self.vlan)
+    }
+}
+
+///
 /// Trait that provides necessary information to indicate a flow (src/flow/mod.rs:20-42); the
-/// default `extract_flow` runs the decode tree on the device.
+/// default `extract_flow` runs the decode tree on the device.  One call per record pays a
+/// host->device->host round trip: for many records use [`extract_flows`] / [`convert_records`],
+/// which take the whole batch in one device call.
 ///
 pub trait FlowExtraction {
     fn payload(&self) -> &[u8];
@@ -57,10 +92,10 @@ pub fn convert_records_in<'b>(input: &'b [u8], records: Vec<PcapRecord<'b>>) -> 
 
 fn convert<'b>(records: Vec<PcapRecord<'b>>, input: Option<&[u8]>) -> Vec<(PcapRecord<'b>, Flow)> {
     let payloads: Vec<&[u8]> = records.iter().map(|r| r.payload).collect();
-    let res = extract_payloads(&payloads, input);
+    let res = flows_only(&payloads, input);
     let mut out = Vec::with_capacity(records.len());
     for (r, f) in records.into_iter().zip(res.into_iter()).rev() {
-        if let Ok(f) = f {
+        if let Some(f) = f {
             out.push((r, f));
         }
     }
@@ -128,14 +163,15 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
 }
 
 /// Row f3 (off the reference's flow path, which never yields a Vxlan flow): for each record, the
-/// outer frame's UDP payload (to `dst_port`, 0 = any; 4789 is the IANA port) parsed as
-/// `layer4::Vxlan::parse(.., endianness)` (src/layer4/vxlan.rs:31-48) and the inner Ethernet
-/// frame's flow, as `<Vxlan as FlowExtraction>::extract_flow` (src/flow/layer4/vxlan.rs:32-50),
-/// with the VXLAN network identifier (0 when the header was not reached).  One device call.
+/// outer frame's UDP payload (to `dst_port`, 0 = any; 4789 is the IANA port) parsed as the
+/// reference's `layer4::Vxlan::parse(.., endianness)` (src/layer4/vxlan.rs:31-48) and the inner
+/// Ethernet frame's flow, as `<Vxlan as FlowExtraction>::extract_flow` (src/flow/layer4/vxlan.rs:
+/// 32-50), with the VXLAN network identifier (0 when the header was not reached).  One device call.
 /// Errors: an outer failure as extract_flow's; an inner Ethernet parse failure as
 /// `Error::L4(Vxlan(NetParser(..)))`; other inner failures as the inner frame's own flow error; a
 /// payload shorter than the VXLAN header as `Error::NetParser(Incomplete)`; an outer flow that is
-/// not UDP to `dst_port` as `Error::NetParser(Custom)`.
+/// not UDP to `dst_port` as `Error::NetParser(Custom)`.  (The payloads of the inner errors are not
+/// computed: sizes 0 / None.)
 pub fn vxlan_flows<'b>(
     input: Option<&'b [u8]>,
     records: &[PcapRecord<'b>],
@@ -174,6 +210,7 @@ pub fn vxlan_flows<'b>(
         let msg = format!("{}", e);
         return (0..n).map(|_| (Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() })), 0)).collect();
     }
+    let outer = details(&payloads, input, &status);
     (0..n)
         .map(|i| {
             let st = status[i];
@@ -183,15 +220,12 @@ pub fn vxlan_flows<'b>(
                     msg: String::from("the outer flow is not UDP to the requested port"),
                 })),
                 ffi::NPR_VXLAN_INCOMPLETE => Err(Error::NetParser(crate::Error::Incomplete { size: None })),
-                s if s > ffi::NPR_VXLAN_INNER => {
-                    let inner = vxlan_inner(payloads[i]);
-                    match s - ffi::NPR_VXLAN_INNER {
-                        1 => Err(vxlan_eth_error(crate::Error::Incomplete { size: None })),
-                        2 => Err(vxlan_eth_error(crate::Error::Failure { msg: String::new() })),
-                        k => Err(flow_error(k, inner)),
-                    }
-                }
-                s => Err(flow_error(s, payloads[i])),
+                s if s > ffi::NPR_VXLAN_INNER => match s - ffi::NPR_VXLAN_INNER {
+                    1 => Err(vxlan_eth_error(crate::Error::Incomplete { size: None })),
+                    2 => Err(vxlan_eth_error(crate::Error::Failure { msg: String::new() })),
+                    k => Err(flow_error(k, 0, &[])),
+                },
+                s => Err(flow_error(s, outer[i], payloads[i])),
             };
             (res, vni[i])
         })
@@ -200,34 +234,12 @@ pub fn vxlan_flows<'b>(
 
 /// Error::L4(Vxlan(NetParser(e))) (src/flow/layer4/vxlan.rs:35-38)
 fn vxlan_eth_error(e: crate::Error) -> Error {
-    let v: layer4::vxlan::errors::Error = layer4::vxlan::errors::Error::NetParser(e);
+    let v = layer4::vxlan::errors::Error::NetParser(e);
     let l4: layer4::errors::Error = v.into();
     Error::L4(l4)
 }
 
-/// The inner Ethernet frame of an Ok outer Ethernet / IP / UDP frame carrying VXLAN: after the
-/// UDP header (8 B) and the VXLAN header (8 B); the L4 header starts 20 bytes into IPv4 (quirk Q7)
-/// and after one byte per extension in IPv6 (quirk Q11).
-fn vxlan_inner(p: &[u8]) -> &[u8] {
-    use crate::layer2::ethernet::{EthernetTypeId, Layer3Id};
-    let (et, l3) = l2_etype(p);
-    let l4 = match et {
-        EthernetTypeId::L3(Layer3Id::IPv6) => {
-            let get = |i: usize| p.get(l3 + i).copied().unwrap_or(0);
-            let mut k = 7;
-            let mut id = get(6);
-            while matches!(id, 0 | 43 | 44 | 50 | 51 | 60) {
-                id = get(k);
-                k += 1;
-            }
-            l3 + k + 33
-        }
-        _ => l3 + 20,
-    };
-    p.get(l4 + 16..).unwrap_or(&[])
-}
-
-// ---- device call ----------------------------------------------------------------------------
+// ---- device calls -----------------------------------------------------------------------------
 /// The buffer and record rows one device call reads: `input` itself when every payload lies
 /// inside it behind its 16-byte record header, else a staged buffer of [16 header bytes | payload]...
 fn stage<'a>(payloads: &[&[u8]], input: Option<&'a [u8]>) -> (Cow<'a, [u8]>, Vec<ffi::npr_record>) {
@@ -270,17 +282,14 @@ fn stage<'a>(payloads: &[&[u8]], input: Option<&'a [u8]>) -> (Cow<'a, [u8]>, Vec
     }
 }
 
-/// One npr_extract_flows call over `payloads` (read from `input` when they lie inside it).
-fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow, Error>> {
+/// One npr_extract_flows call: per payload Some(flow) or None, and the status codes.
+fn extract_raw(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<(Vec<Option<Flow>>, Vec<u8>), crate::Error> {
     let n = payloads.len();
-    if n == 0 {
-        return Vec::new();
-    }
     let (buf, recs) = stage(payloads, input);
     let mut flows = vec![ffi::npr_flow::default(); n];
     let mut flows6 = vec![ffi::npr_flow_v6::default(); n];
     let mut status = vec![0u8; n];
-    let r = with_ctx(|ctx| {
+    with_ctx(|ctx| {
         let st = unsafe {
             ffi::npr_extract_flows(
                 ctx,
@@ -294,13 +303,77 @@ fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow
             )
         };
         check(ctx, st)
-    });
-    if let Err(e) = r {
-        let msg = format!("{}", e);
-        return (0..n).map(|_| Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() }))).collect();
+    })?;
+    let out = (0..n).map(|i| if status[i] == 0 { Some(to_flow(&flows[i], &flows6[i])) } else { None }).collect();
+    Ok((out, status))
+}
+
+/// The error payloads (npr_flow_details) of the payloads whose status is not Ok: one more device
+/// call over those records only (0 where none was computed).
+fn details(payloads: &[&[u8]], input: Option<&[u8]>, status: &[u8]) -> Vec<u64> {
+    let n = payloads.len();
+    let mut det = vec![0u64; n];
+    let bad: Vec<usize> = (0..n).filter(|&i| status[i] != 0 && status[i] < ffi::NPR_VXLAN_NOT_UDP).collect();
+    if bad.is_empty() {
+        return det;
     }
-    (0..n)
-        .map(|i| if status[i] == 0 { Ok(to_flow(&flows[i], &flows6[i])) } else { Err(flow_error(status[i], payloads[i])) })
+    let sub: Vec<&[u8]> = bad.iter().map(|&i| payloads[i]).collect();
+    let (buf, recs) = stage(&sub, input);
+    let mut got = vec![0u64; sub.len()];
+    let r = with_ctx(|ctx| {
+        let st = unsafe {
+            ffi::npr_flow_details(
+                ctx,
+                buf.as_ptr(),
+                buf.len(),
+                recs.as_ptr(),
+                sub.len(),
+                std::ptr::null_mut(),
+                got.as_mut_ptr(),
+            )
+        };
+        check(ctx, st)
+    });
+    if r.is_ok() {
+        for (k, &i) in bad.iter().enumerate() {
+            det[i] = got[k];
+        }
+    }
+    det
+}
+
+fn flows_only(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Option<Flow>> {
+    if payloads.is_empty() {
+        return Vec::new();
+    }
+    match extract_raw(payloads, input) {
+        Ok((f, _)) => f,
+        Err(_) => vec![None; payloads.len()],
+    }
+}
+
+/// extract_flow over `payloads` (read from `input` when they lie inside it): one device call, plus
+/// one for the error payloads of the records that failed.
+fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow, Error>> {
+    let n = payloads.len();
+    if n == 0 {
+        return Vec::new();
+    }
+    let (flows, status) = match extract_raw(payloads, input) {
+        Ok(v) => v,
+        Err(e) => {
+            let msg = format!("{}", e);
+            return (0..n).map(|_| Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() }))).collect();
+        }
+    };
+    let det = details(payloads, input, &status);
+    flows
+        .into_iter()
+        .enumerate()
+        .map(|(i, f)| match f {
+            Some(f) => Ok(f),
+            None => Err(flow_error(status[i], det[i], payloads[i])),
+        })
         .collect()
 }
 
@@ -322,85 +395,58 @@ fn to_flow(f: &ffi::npr_flow, f6: &ffi::npr_flow_v6) -> Flow {
     }
 }
 
-// ---- npr_flow_status -> the reference's flow error tree ------------------------------------------
-/// The first EtherType after the 802.1Q/ad tags (src/layer2/ethernet.rs:163-216), as the
-/// reference's EthernetTypeId: only LLDP / an 802.3 length reach flow status 3.
-fn l2_etype(p: &[u8]) -> (crate::layer2::ethernet::EthernetTypeId, usize) {
-    use crate::layer2::ethernet::{EthernetTypeId, Layer3Id, VlanTypeId};
-    let mut pos = 12;
-    loop {
-        if p.len() < pos + 2 {
-            return (EthernetTypeId::PayloadLength(0), pos);
-        }
-        let t = u16::from_be_bytes([p[pos], p[pos + 1]]);
-        match t {
-            0x8100 | 0x88a8 => pos += 4,
-            0x88cc => return (EthernetTypeId::L3(Layer3Id::Lldp), pos + 2),
-            0x0800 => return (EthernetTypeId::L3(Layer3Id::IPv4), pos + 2),
-            0x86dd => return (EthernetTypeId::L3(Layer3Id::IPv6), pos + 2),
-            0x0806 => return (EthernetTypeId::L3(Layer3Id::Arp), pos + 2),
-            x if x <= 1500 => return (EthernetTypeId::PayloadLength(x), pos + 2),
-            _ => return (EthernetTypeId::Vlan(VlanTypeId::VlanTagId), pos + 2),
-        }
-    }
+// ---- npr_flow_status + npr_flow_details -> the reference's flow error tree ----------------------------
+/// nom's message for a map_opt! / map_res! failure: "Error: " + the Debug form of
+/// Context::Code(<the failing primitive's input>, kind) (src/errors.rs:43-47); the detail word holds
+/// the input's frame offsets start | end << 32.
+fn nom_failure(p: &[u8], det: u64, kind: nom::ErrorKind<u32>) -> crate::Error {
+    let (a, b) = ((det & 0xffff_ffff) as usize, (det >> 32) as usize);
+    let input = if a <= b && b <= p.len() { &p[a..b] } else { &[][..] };
+    crate::Error::Failure { msg: format!("Error: {:?}", nom::Context::Code(input, kind)) }
 }
 
-/// The L3 protocol id the reference rejects at flow status 15 / 16 (src/layer3/ipv4.rs:119,
-/// src/layer3/ipv6.rs:29-56: one next-header byte per extension).
-fn l3_proto(p: &[u8], v6: bool) -> crate::layer3::InternetProtocolId {
-    use crate::layer3::InternetProtocolId;
-    let (_, l3) = l2_etype(p);
-    let get = |i: usize| p.get(l3 + i).copied().unwrap_or(0);
-    let mut id = if v6 { get(6) } else { get(9) };
-    if v6 {
-        let mut k = 7;
-        while matches!(id, 0 | 43 | 44 | 50 | 51 | 60) {
-            id = get(k);
-            k += 1;
-        }
-    }
-    InternetProtocolId::new(id).unwrap_or(InternetProtocolId::ICMP)
-}
-
-fn flow_error(st: u8, p: &[u8]) -> Error {
+fn flow_error(st: u8, det: u64, p: &[u8]) -> Error {
     use crate::layer2::ethernet::{EthernetTypeId as E, Layer3Id as L3};
     use crate::layer3::InternetProtocolId as P;
     use layer2::ethernet::errors::Error as Eth;
     use layer3::{arp, ipv4, ipv6};
     type NP = crate::Error;
-    let inc = || NP::Incomplete { size: None };
-    let fail = || NP::Failure { msg: String::new() };
-    let cust = || NP::Custom { msg: String::new() };
+    let inc = || NP::Incomplete { size: Some(det as usize) };
+    let opt = || nom_failure(p, det, nom::ErrorKind::MapOpt);
     let eth = |e: Eth| -> Error {
         let l2: layer2::errors::Error = e.into();
         l2.into()
     };
     let l3e = |e: layer3::errors::Error| -> Error { e.into() };
+    let v4 = || E::L3(L3::IPv4);
+    let v6 = || E::L3(L3::IPv6);
+    let proto = || P::new(det as u8).unwrap_or(P::ICMP);
+    let size = det as usize;
     match st {
         1 => Error::NetParser(inc()),
-        2 => Error::NetParser(fail()),
-        3 => eth(Eth::EthernetType { etype: l2_etype(p).0 }),
-        4 => eth(Eth::NetParser { l3: E::L3(L3::IPv4), err: inc() }),
-        5 => eth(Eth::NetParser { l3: E::L3(L3::IPv4), err: fail() }),
-        6 => eth(Eth::NetParser { l3: E::L3(L3::IPv4), err: cust() }),
-        7 => eth(Eth::NetParser { l3: E::L3(L3::IPv6), err: inc() }),
-        8 => eth(Eth::NetParser { l3: E::L3(L3::IPv6), err: fail() }),
-        9 => eth(Eth::NetParser { l3: E::L3(L3::IPv6), err: cust() }),
+        2 => Error::NetParser(opt()),
+        3 => eth(Eth::EthernetType { etype: E::from_value(det as u16).unwrap_or(E::PayloadLength(0)) }),
+        4 => eth(Eth::NetParser { l3: v4(), err: inc() }),
+        5 => eth(Eth::NetParser { l3: v4(), err: opt() }),
+        6 => eth(Eth::NetParser { l3: v4(), err: NP::Custom { msg: format!("Expected version 4, was {}", det) } }),
+        7 => eth(Eth::NetParser { l3: v6(), err: inc() }),
+        8 => eth(Eth::NetParser { l3: v6(), err: opt() }),
+        9 => eth(Eth::NetParser { l3: v6(), err: NP::Custom { msg: format!("Expected version 6, version was {}", det) } }),
         10 => eth(Eth::NetParser { l3: E::L3(L3::Arp), err: inc() }),
-        11 => eth(Eth::Incomplete { l3: E::L3(L3::IPv4), size: 0 }),
-        12 => eth(Eth::Incomplete { l3: E::L3(L3::IPv6), size: 0 }),
-        13 => eth(Eth::Incomplete { l3: E::L3(L3::Arp), size: 0 }),
+        11 => eth(Eth::Incomplete { l3: v4(), size }),
+        12 => eth(Eth::Incomplete { l3: v6(), size }),
+        13 => eth(Eth::Incomplete { l3: E::L3(L3::Arp), size }),
         14 => l3e(arp::errors::Error::Flow.into()),
-        15 => l3e(ipv4::errors::Error::InternetProtocolId { id: l3_proto(p, false) }.into()),
-        16 => l3e(ipv6::errors::Error::InternetProtocolId { id: l3_proto(p, true) }.into()),
+        15 => l3e(ipv4::errors::Error::InternetProtocolId { id: proto() }.into()),
+        16 => l3e(ipv6::errors::Error::InternetProtocolId { id: proto() }.into()),
         17 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: inc() }.into()),
-        18 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: fail() }.into()),
+        18 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: nom_failure(p, det, nom::ErrorKind::MapRes) }.into()),
         19 => l3e(ipv4::errors::Error::NetParser { l4: P::Udp, err: inc() }.into()),
         20 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: inc() }.into()),
-        21 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: fail() }.into()),
+        21 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: nom_failure(p, det, nom::ErrorKind::MapRes) }.into()),
         22 => l3e(ipv6::errors::Error::NetParser { l4: P::Udp, err: inc() }.into()),
-        23 => l3e(ipv4::errors::Error::Incomplete { l4: P::Udp, size: 0 }.into()),
-        24 => l3e(ipv6::errors::Error::Incomplete { l4: P::Udp, size: 0 }.into()),
+        23 => l3e(ipv4::errors::Error::Incomplete { l4: P::Udp, size }.into()),
+        24 => l3e(ipv6::errors::Error::Incomplete { l4: P::Udp, size }.into()),
         _ => Error::NetParser(NP::Custom { msg: format!("record not inside the buffer (status {})", st) }),
     }
 }

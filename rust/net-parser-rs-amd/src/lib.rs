@@ -1,4 +1,5 @@
-//! net-parser-rs-amd — a drop-in for net-parser-rs 0.3 whose hot path runs on an AMD MI355X.
+//! net-parser-rs-amd — a drop-in for net-parser-rs 0.3 whose record parse and flow extraction run
+//! on an AMD MI355X (HIP kernels in libnpr.so, behind the C-ABI of include/npr.h).
 //!
 //! Switch a dependent crate over by renaming the dependency:
 //!
@@ -7,32 +8,42 @@
 //! net-parser-rs = { package = "net-parser-rs-amd", path = ".../rust/net-parser-rs-amd" }
 //! ```
 //!
-//! and code written against the reference compiles unchanged:
+//! and code written against the reference compiles unchanged.  The reference crate is neither a
+//! dependency nor linked: its public types are restated in this crate (`types.rs`, field for field,
+//! same `Display` strings) and every parse runs in libnpr.
 //!
-//! | reference (src file:line)                          | here                                         |
-//! |----------------------------------------------------|----------------------------------------------|
-//! | `net_parser_rs::parse` (src/lib.rs:44-46)          | [`parse`]: device record chain                |
-//! | `CaptureFile::parse` (src/file.rs:14-35)           | [`CaptureFile::parse`]                        |
-//! | `PcapRecords::parse` (src/record.rs:21-54)         | [`PcapRecords::parse`]: `npr_records_parse`   |
-//! | `PcapRecord::parse` (src/record.rs:102-121)        | the reference's own (16 B, host side)         |
-//! | `GlobalHeader::parse` (src/global_header.rs:40-70) | the reference's own (24 B, host side)         |
-//! | `FlowExtraction::extract_flow` (src/flow/mod.rs:23)| [`flow::FlowExtraction`]: `npr_extract_flows` |
-//! | `flow::convert_records` (src/flow/mod.rs:101-123)  | [`flow::convert_records`]                     |
-//! | README `CaptureParser` facade (README.md:17-28)    | [`CaptureParser`]                             |
-//!
-//! Every type whose fields are public (`GlobalHeader`, `PcapRecord`, `Error`, `flow::Flow`,
-//! `flow::device::Device`, `flow::info`, `flow::errors`, `common::MacAddress`, the layer id
-//! enums) IS the reference crate's type, re-exported.  `CaptureFile` and `PcapRecords` are
-//! redefined with the same public API because the reference's `PcapRecords` has a private field.
+//! | reference (src file:line)                          | here                                            |
+//! |----------------------------------------------------|-------------------------------------------------|
+//! | `net_parser_rs::parse` (src/lib.rs:44-46)          | [`parse`]                                       |
+//! | `CaptureFile::parse` (src/file.rs:14-35)           | [`CaptureFile::parse`]                          |
+//! | `GlobalHeader::parse` (src/global_header.rs:40-70) | `npr_global_header_parse` (24 B, host side)     |
+//! | `PcapRecords::parse` (src/record.rs:21-54)         | `npr_records_parse`: the record chain on the GPU |
+//! | `PcapRecord::parse` (src/record.rs:102-121)        | `npr_record_parse` (16 B, host side)            |
+//! | `FlowExtraction::extract_flow` (src/flow/mod.rs:23)| [`flow::FlowExtraction`]: `npr_extract_flows`   |
+//! | `flow::convert_records` (src/flow/mod.rs:101-123)  | [`flow::convert_records`]                       |
+//! | README `CaptureParser` facade (README.md:17-28)    | [`CaptureParser`]                               |
 //!
 //! Device errors (no GPU, a HIP failure) surface as `Error::Custom { msg }`: the reference's
 //! error enum (src/errors.rs:3-11) has no variant for them.
+//!
+//! Threading: the reference's functions are pure and reentrant (its errors are Send + Sync,
+//! src/errors.rs:13-14).  Here every thread uses its own libnpr context (`thread_local!` below),
+//! and libnpr orders the look-back launches of all contexts on a device, so any number of threads
+//! may call in at once.
 #![allow(clippy::needless_lifetimes)]
 
 pub mod ffi;
 pub mod flow;
+mod types;
 
-/// Path compatibility with `net_parser_rs::record::*` and `net_parser_rs::file::*`.
+pub use types::{common, errors, layer2, layer3, layer4};
+
+/// src/global_header.rs: the header type, its constants and GlobalHeader::parse (over the C-ABI)
+pub mod global_header {
+    pub use crate::types::global_header::{GlobalHeader, NATIVE_ENDIAN};
+}
+
+/// src/record.rs and src/file.rs paths
 pub mod record {
     pub use crate::{PcapRecord, PcapRecords};
 }
@@ -40,13 +51,14 @@ pub mod file {
     pub use crate::CaptureFile;
 }
 
-pub use net_parser_rs::{common, errors, global_header, layer2, layer3, layer4};
-pub use net_parser_rs::{Error, GlobalHeader, PcapRecord};
+pub use errors::Error;
+pub use global_header::GlobalHeader;
 
 use std::cell::RefCell;
 use std::ffi::CStr;
+use std::time::{Duration, SystemTime, UNIX_EPOCH};
 
-// ---- one libnpr context per thread (npr_ctx is per thread; the reference is reentrant) -------
+// ---- one libnpr context per thread ----------------------------------------------------------------
 struct Ctx(*mut ffi::npr_ctx);
 
 impl Drop for Ctx {
@@ -82,7 +94,7 @@ where
     })
 }
 
-/// An npr_status as the reference's crate::errors::Error (codes 1..3 map 1:1, src/errors.rs:3-11).
+/// A device-path npr_status as crate::errors::Error (codes 1..3 map 1:1, src/errors.rs:3-11).
 pub(crate) fn check(ctx: *mut ffi::npr_ctx, st: ffi::npr_status) -> Result<(), Error> {
     match st {
         ffi::NPR_OK => Ok(()),
@@ -90,7 +102,11 @@ pub(crate) fn check(ctx: *mut ffi::npr_ctx, st: ffi::npr_status) -> Result<(), E
         ffi::NPR_FAILURE => Err(Error::Failure { msg: String::new() }),
         ffi::NPR_CUSTOM => Err(Error::Custom { msg: String::new() }),
         _ => {
-            let m = unsafe { CStr::from_ptr(ffi::npr_ctx_last_error(ctx)) }.to_string_lossy().into_owned();
+            let m = if ctx.is_null() {
+                String::new()
+            } else {
+                unsafe { CStr::from_ptr(ffi::npr_ctx_last_error(ctx)) }.to_string_lossy().into_owned()
+            };
             Err(Error::Custom { msg: format!("npr status {}: {}", st, m) })
         }
     }
@@ -103,7 +119,114 @@ pub(crate) fn endian(e: nom::Endianness) -> std::os::raw::c_int {
     }
 }
 
-/// A device record row as the reference's PcapRecord borrowing `input` (src/record.rs:88-100).
+/// nom's Needed::Size for an input of `have` bytes that stops a chain of fixed-size primitives
+/// (`sizes`, in parse order): the size of the first primitive that does not fit (nom 4.2 reports a
+/// primitive's full size, e.g. u32! -> 4).
+pub(crate) fn needed(sizes: &[usize], have: usize) -> Option<usize> {
+    let mut end = 0;
+    for &k in sizes {
+        end += k;
+        if end > have {
+            return Some(k);
+        }
+    }
+    None
+}
+
+// ---- GlobalHeader::parse (src/global_header.rs:40-70) over npr_global_header_parse -----------------
+impl GlobalHeader {
+    /// The 24-byte libpcap file header: the magic read in native order decides the endianness
+    /// (0xA1B2C3D4: native, anything else: the other order), then six fields in that order.
+    pub fn parse<'a>(input: &'a [u8]) -> Result<(&'a [u8], GlobalHeader), Error> {
+        let mut h = ffi::npr_global_header::default();
+        let mut used = 0usize;
+        let st = unsafe { ffi::npr_global_header_parse(input.as_ptr(), input.len(), &mut h, &mut used) };
+        if st == ffi::NPR_INCOMPLETE {
+            // u32! magic, u16! x2, i32! x2, u32! x2 (src/global_header.rs:43-59)
+            return Err(Error::Incomplete { size: needed(&[4, 2, 2, 4, 4, 4, 4], input.len()) });
+        }
+        check(std::ptr::null_mut(), st)?;
+        let header = GlobalHeader {
+            endianness: if h.endianness == ffi::NPR_BIG { nom::Endianness::Big } else { nom::Endianness::Little },
+            version_major: h.version_major,
+            version_minor: h.version_minor,
+            zone: h.zone,
+            sig_figs: h.sig_figs,
+            snap_length: h.snap_length,
+            network: h.network,
+        };
+        Ok((&input[used..], header))
+    }
+}
+
+// ---- PcapRecord (src/record.rs:56-139) ------------------------------------------------------------
+/// One libpcap record: its header fields and the payload it borrows from the input
+#[derive(Clone, Copy, Debug)]
+pub struct PcapRecord<'a> {
+    pub timestamp: SystemTime,
+    pub actual_length: u32,
+    pub original_length: u32,
+    pub payload: &'a [u8],
+}
+
+impl<'a> Default for PcapRecord<'a> {
+    fn default() -> Self {
+        PcapRecord { timestamp: UNIX_EPOCH, actual_length: 0, original_length: 0, payload: &[] }
+    }
+}
+
+impl<'a> PcapRecord<'a> {
+    /// UNIX_EPOCH + seconds + microseconds (the microseconds are not bounded, src/record.rs:82-86)
+    pub fn convert_packet_time(ts_seconds: u32, ts_microseconds: u32) -> SystemTime {
+        UNIX_EPOCH + Duration::from_secs(ts_seconds as u64) + Duration::from_micros(ts_microseconds as u64)
+    }
+
+    pub fn new(timestamp: SystemTime, actual_length: u32, original_length: u32, payload: &'a [u8]) -> PcapRecord<'a> {
+        PcapRecord { timestamp, actual_length, original_length, payload }
+    }
+
+    /// One record (16-byte header in `endianness`, then `actual_length` payload bytes) and the
+    /// rest of the input, by npr_record_parse.
+    pub fn parse<'b>(input: &'b [u8], endianness: nom::Endianness) -> Result<(&'b [u8], PcapRecord<'b>), Error> {
+        let mut r = ffi::npr_record::default();
+        let mut used = 0usize;
+        let st = unsafe { ffi::npr_record_parse(input.as_ptr(), input.len(), endian(endianness), &mut r, &mut used) };
+        if st == ffi::NPR_INCOMPLETE {
+            // four u32! then take!(actual_length) (src/record.rs:106-111)
+            let size = if input.len() < 16 {
+                needed(&[4, 4, 4, 4], input.len())
+            } else {
+                let b = [input[8], input[9], input[10], input[11]];
+                let incl = match endianness {
+                    nom::Endianness::Big => u32::from_be_bytes(b),
+                    nom::Endianness::Little => u32::from_le_bytes(b),
+                };
+                Some(incl as usize)
+            };
+            return Err(Error::Incomplete { size });
+        }
+        check(std::ptr::null_mut(), st)?;
+        Ok((&input[used..], to_record(input, &r)))
+    }
+}
+
+impl<'a> std::fmt::Display for PcapRecord<'a> {
+    /// `Timestamp=<secs><millis>   Length=..   Original Length=..` (src/record.rs:123-139: the
+    /// milliseconds are appended without padding)
+    fn fmt(&self, f: &mut std::fmt::Formatter) -> std::fmt::Result {
+        let d = self.timestamp.duration_since(UNIX_EPOCH).map_err(|_| std::fmt::Error)?;
+        write!(
+            f,
+            "Timestamp={}{}   Length={}   Original Length={}",
+            d.as_secs(),
+            d.subsec_millis(),
+            self.actual_length,
+            self.original_length
+        )
+    }
+}
+
+/// A device record row as a PcapRecord borrowing `input`.
 pub(crate) fn to_record<'b>(input: &'b [u8], r: &ffi::npr_record) -> PcapRecord<'b> {
     let o = r.offset as usize + 16;
     PcapRecord::new(
@@ -114,7 +237,7 @@ pub(crate) fn to_record<'b>(input: &'b [u8], r: &ffi::npr_record) -> PcapRecord<
     )
 }
 
-// ---- PcapRecords (src/record.rs:7-54) ----------------------------------------------------------
+// ---- PcapRecords (src/record.rs:7-54) -------------------------------------------------------------
 /// Collection of pcap records associated with a libpcap capture
 #[derive(Clone, Debug)]
 pub struct PcapRecords<'a> {
@@ -130,9 +253,9 @@ impl<'a> PcapRecords<'a> {
         self.inner
     }
 
-    /// Records of `input` (no global header) in the given endianness, until the first
-    /// incomplete record (src/record.rs:30-49); the remainder is returned like the reference's.
-    /// The record chain is found and verified on the device (npr_records_parse).
+    /// Records of `input` (no global header) in the given endianness, until the first incomplete
+    /// record (src/record.rs:30-49); the remainder is returned like the reference's.  The record
+    /// chain is found and verified on the device (npr_records_parse).
     pub fn parse<'b>(input: &'b [u8], endianness: nom::Endianness) -> Result<(&'b [u8], PcapRecords<'b>), Error> {
         let (rows, consumed) = with_ctx(|ctx| {
             let cap = input.len() / 16 + 1;
@@ -159,7 +282,7 @@ impl<'a> PcapRecords<'a> {
     }
 }
 
-// ---- CaptureFile (src/file.rs:4-35) -------------------------------------------------------------
+// ---- CaptureFile (src/file.rs:4-35) ---------------------------------------------------------------
 #[derive(Clone, Debug)]
 pub struct CaptureFile<'a> {
     pub global_header: GlobalHeader,
@@ -168,8 +291,8 @@ pub struct CaptureFile<'a> {
 
 impl<'a> CaptureFile<'a> {
     ///
-    /// Parse a slice of bytes that start with libpcap file format header: the 24-byte header on
-    /// the host (the reference's own GlobalHeader::parse), the record chain on the device.
+    /// Parse a slice of bytes that start with libpcap file format header: the 24-byte header on the
+    /// host (npr_global_header_parse), the record chain on the device.
     ///
     pub fn parse<'b>(input: &'b [u8]) -> Result<(&'b [u8], CaptureFile<'b>), Error> {
         let (rem, header) = GlobalHeader::parse(input)?;

@@ -1,9 +1,12 @@
-//! `cargo test` on a machine with an MI355X: this crate against the reference crate itself
-//! (net-parser-rs 0.3, a dependency) on the same capture bytes.
+//! `cargo test` on a machine with an MI355X: this crate against the reference crate (net-parser-rs
+//! 0.3, a dev-dependency: the checker only, never linked into the library) on the same capture
+//! bytes.  The types are separate restatements, so results are compared through their `Debug` and
+//! `Display` forms, which the restatement keeps identical.
 use net_parser_rs_amd as amd;
 
-/// A little-endian capture: Eth/IPv4/TCP and Eth/IPv4/UDP records, one ARP record (never a
-/// flow), one VLAN-tagged record and a truncated tail (the chain stops before it, Q3).
+/// A little-endian capture: Eth/IPv4/TCP and Eth/IPv4/UDP records, ARP records (never a flow),
+/// VLAN-tagged records, frames cut short, wrong UDP lengths, unknown protocols, and a truncated
+/// tail (the chain stops before it, Q3).
 fn capture() -> Vec<u8> {
     let mut v = vec![0xd4, 0xc3, 0xb2, 0xa1, 2, 0, 4, 0];
     v.extend_from_slice(&[0u8; 8]);
@@ -19,23 +22,28 @@ fn capture() -> Vec<u8> {
             f.extend_from_slice(&[1u8; 28]);
         } else {
             let udp = i % 2 == 1;
+            let proto = if i % 13 == 6 { 47 } else if udp { 17 } else { 6 };
             f.extend_from_slice(&[0x08, 0x00, 0x45, 0x00]);
             let l4len: u16 = if udp { 8 + 12 } else { 20 + 10 };
             f.extend_from_slice(&(20 + l4len).to_be_bytes());
-            f.extend_from_slice(&[0, 0, 0, 0, 64, if udp { 17 } else { 6 }, 0, 0]);
+            f.extend_from_slice(&[0, 0, 0, 0, 64, proto, 0, 0]);
             f.extend_from_slice(&[10, 0, (i >> 8) as u8, i as u8, 192, 168, 1, (i % 250) as u8]);
             f.extend_from_slice(&((1000 + i) as u16).to_be_bytes());
             f.extend_from_slice(&80u16.to_be_bytes());
             if udp {
-                f.extend_from_slice(&l4len.to_be_bytes());
+                let ul = if i % 17 == 9 { l4len - 3 } else { l4len };
+                f.extend_from_slice(&ul.to_be_bytes());
                 f.extend_from_slice(&[0u8; 2]);
                 f.extend_from_slice(&[9u8; 12]);
             } else {
                 f.extend_from_slice(&[0u8; 8]);
-                f.extend_from_slice(&[0x50, 0x18]);
+                f.extend_from_slice(&[if i % 19 == 4 { 0x20 } else { 0x50 }, 0x18]);
                 f.extend_from_slice(&[0u8; 6]);
                 f.extend_from_slice(&[7u8; 10]);
             }
+        }
+        if i % 23 == 8 {
+            f.truncate(f.len() * (i as usize % 5) / 5); // a frame cut short: every Incomplete step
         }
         v.extend_from_slice(&(1_600_000_000 + i / 1000).to_le_bytes());
         v.extend_from_slice(&(i % 1_000_000).to_le_bytes());
@@ -47,12 +55,13 @@ fn capture() -> Vec<u8> {
     v
 }
 
-fn same_record(a: &net_parser_rs::PcapRecord, b: &net_parser_rs::PcapRecord) -> bool {
+fn same_record(a: &amd::PcapRecord, b: &net_parser_rs::PcapRecord) -> bool {
     a.timestamp == b.timestamp
         && a.actual_length == b.actual_length
         && a.original_length == b.original_length
         && a.payload.as_ptr() == b.payload.as_ptr()
         && a.payload.len() == b.payload.len()
+        && format!("{}", a) == format!("{}", b)
 }
 
 #[test]
@@ -61,9 +70,31 @@ fn capture_file_parse_matches_reference() {
     let (rem_a, fa) = amd::parse(&data).expect("device parse");
     let (rem_r, fr) = net_parser_rs::parse(&data).expect("reference parse");
     assert_eq!(rem_a.len(), rem_r.len());
+    assert_eq!(format!("{:?}", fa.global_header), format!("{:?}", fr.global_header));
     assert_eq!(fa.records.len(), fr.records.len());
     let (ra, rr) = (fa.records.into_inner(), fr.records.into_inner());
     assert!(ra.iter().zip(rr.iter()).all(|(a, b)| same_record(a, b)));
+}
+
+#[test]
+fn single_object_parsers_match_reference_on_every_prefix() {
+    // GlobalHeader::parse / PcapRecord::parse over truncated inputs: the same Ok values, the same
+    // Incomplete { size } (npr_global_header_parse / npr_record_parse + nom's Needed sizes)
+    let data = capture();
+    for k in 0..=40 {
+        let a = amd::GlobalHeader::parse(&data[..k]);
+        let r = net_parser_rs::GlobalHeader::parse(&data[..k]);
+        assert_eq!(format!("{:?}", a), format!("{:?}", r), "header prefix {}", k);
+    }
+    for big in [false, true].iter() {
+        let e = if *big { nom::Endianness::Big } else { nom::Endianness::Little };
+        for k in 0..=120 {
+            let s = &data[24..24 + k];
+            let a = amd::PcapRecord::parse(s, e).map(|(rem, r)| (rem.len(), format!("{} {:?}", r, r.payload)));
+            let r = net_parser_rs::PcapRecord::parse(s, e).map(|(rem, r)| (rem.len(), format!("{} {:?}", r, r.payload)));
+            assert_eq!(format!("{:?}", a), format!("{:?}", r), "record prefix {} big {}", k, big);
+        }
+    }
 }
 
 #[test]
@@ -76,29 +107,37 @@ fn convert_records_matches_reference() {
     assert_eq!(a.len(), r.len());
     for ((ra, fa), (rr, fr)) in a.iter().zip(r.iter()) {
         assert!(same_record(ra, rr));
-        assert_eq!(fa, fr);
+        assert_eq!(format!("{:?}", fa), format!("{:?}", fr));
+        assert_eq!(format!("{}", fa), format!("{}", fr));
     }
     let (_, fa2) = amd::parse(&data).unwrap();
     let b = amd::flow::convert_records_in(&data, fa2.records.into_inner());
-    assert!(b.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && same_record(&x.0, &y.0)));
+    assert!(b.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && x.0.payload.as_ptr() == y.0.payload.as_ptr()));
     let (rem, c) = amd::flow::parse_and_convert(&data).unwrap();
     assert_eq!(rem.len(), 3);
-    assert!(c.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && same_record(&x.0, &y.0)));
+    assert!(c.iter().zip(a.iter()).all(|(x, y)| x.1 == y.1 && x.0.payload.as_ptr() == y.0.payload.as_ptr()));
 }
 
 #[test]
-fn extract_flow_errors_take_the_reference_variant() {
+fn extract_flow_results_and_errors_equal_the_reference() {
+    // every record: Ok flows equal, errors equal in variant, payload (sizes, ids, positions) and
+    // message, through Debug and Display
     use amd::flow::FlowExtraction as _;
+    use net_parser_rs::flow::FlowExtraction as _;
     let data = capture();
+    let (_, fa) = amd::parse(&data).unwrap();
     let (_, fr) = net_parser_rs::parse(&data).unwrap();
-    for r in fr.records.into_inner().iter().take(40) {
-        let a = amd::flow::FlowExtraction::extract_flow(r);
-        let b = net_parser_rs::flow::FlowExtraction::extract_flow(r);
-        match (a, b) {
-            (Ok(x), Ok(y)) => assert_eq!(x, y),
-            (Err(x), Err(y)) => assert_eq!(format!("{:?}", x).split('{').next(), format!("{:?}", y).split('{').next()),
-            (x, y) => panic!("{:?} vs {:?}", x, y),
+    let ra = fa.records.into_inner();
+    let rr = fr.records.into_inner();
+    let batch = amd::flow::extract_flows(&ra);
+    for (i, (a, r)) in ra.iter().zip(rr.iter()).enumerate().take(1500) {
+        let x = a.extract_flow();
+        let y = r.extract_flow();
+        assert_eq!(format!("{:?}", x), format!("{:?}", y), "record {}", i);
+        if let (Err(x), Err(y)) = (&x, &y) {
+            assert_eq!(format!("{}", x), format!("{}", y), "record {}", i);
         }
+        assert_eq!(format!("{:?}", batch[i]), format!("{:?}", y), "record {} (batch)", i);
     }
 }
 
@@ -111,6 +150,32 @@ fn readme_facade() {
     use amd::flow::*;
     let flow = packet.extract_flow().expect("Could not extract flow");
     assert_eq!(flow.destination.port, 80);
+}
+
+#[test]
+fn concurrent_threads() {
+    // reentrant like the reference: several threads parse and convert at once (each its own context)
+    let data = std::sync::Arc::new(capture());
+    let want = {
+        let (_, f) = net_parser_rs::parse(&data).unwrap();
+        net_parser_rs::flow::convert_records(f.records.into_inner()).len()
+    };
+    let hs: Vec<_> = (0..4)
+        .map(|_| {
+            let d = data.clone();
+            std::thread::spawn(move || {
+                (0..20)
+                    .map(|_| {
+                        let (_, f) = amd::parse(&d).unwrap();
+                        amd::flow::convert_records(f.records.into_inner()).len()
+                    })
+                    .collect::<Vec<_>>()
+            })
+        })
+        .collect();
+    for h in hs {
+        assert!(h.join().unwrap().iter().all(|&k| k == want));
+    }
 }
 
 /// Eth/IPv4/UDP to 4789 carrying VXLAN + an inner Eth/IPv4/TCP frame, every 3rd record a
@@ -174,7 +239,7 @@ fn vxlan_inner_flows_match_reference() {
                 assert_eq!(*vni, vx.network_identifier, "record {}", i);
                 let (_, l2) = net_parser_rs::layer2::ethernet::Ethernet::parse(vx.payload).unwrap();
                 let want = l2.extract_flow().unwrap();
-                assert_eq!(res.as_ref().unwrap(), &want, "record {}", i);
+                assert_eq!(format!("{:?}", res.as_ref().unwrap()), format!("{:?}", want), "record {}", i);
             }
         }
     }

@@ -70,6 +70,8 @@ def lib():
         L.or_convert_records.restype = _sz
         L.or_extract_flows.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp, _vp]
         L.or_extract_flows.restype = None
+        L.or_flow_details.argtypes = [_vp, _sz, _vp, _sz, _vp, _vp]
+        L.or_flow_details.restype = None
         L.or_vxlan_flows.argtypes = [_vp, _sz, _vp, _sz, ctypes.c_uint32, ctypes.c_int, _vp, _vp, _vp, _vp]
         L.or_vxlan_flows.restype = None
         L.or_vxlan_parse.argtypes = [_vp, _sz, ctypes.c_int, ctypes.POINTER(OrVxlan)]
@@ -150,6 +152,17 @@ def extract_flows(data, records):
     st = np.zeros(n, dtype=np.uint8)
     lib().or_extract_flows(p, a.size, recs.ctypes.data, n, flows.ctypes.data, v6.ctypes.data, st.ctypes.data)
     return flows, v6, st
+
+
+def flow_details(data, records):
+    """Per-record status and error payload (include/npr.h npr_flow_details): (status, detail)."""
+    a, p = _buf(data)
+    n = len(records)
+    recs = np.ascontiguousarray(records, dtype=_abi.RECORD_DTYPE)
+    st = np.zeros(n, dtype=np.uint8)
+    det = np.zeros(n, dtype=np.uint64)
+    lib().or_flow_details(p, a.size, recs.ctypes.data, n, st.ctypes.data, det.ctypes.data)
+    return st, det
 
 
 def vxlan_flows(data, records, dst_port=0, big=True):

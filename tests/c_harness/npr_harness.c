@@ -104,6 +104,15 @@ static void run(npr_ctx *ctx, const char *path) {
   for (size_t i = 0; i < on; ++i)
     if (st[i] == NPR_FLOW_OK && memcmp(&fl[i], &dfl[i], sizeof *fl)) ++k;
   CHECK(k == 0, "%s: %zu dense flows differ", path, k);
+  /* the error payloads the crate puts into the reference's error variants */
+  uint64_t *det = calloc(cap, sizeof *det), *odet = calloc(cap, sizeof *odet);
+  uint8_t *dst_ = calloc(cap, 1);
+  or_flow_details(in, len, orec, on, ost, odet);
+  CHECK(npr_flow_details(ctx, in, len, orec, on, dst_, det) == NPR_OK, "%s: flow_details", path);
+  CHECK(!memcmp(dst_, ost, on) && !memcmp(det, odet, on * sizeof *det), "%s: flow error details", path);
+  free(det);
+  free(odet);
+  free(dst_);
 
   /* flow::convert_records (src/flow/mod.rs:101-123) */
   size_t nf = 0;

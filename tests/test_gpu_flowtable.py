@@ -106,3 +106,30 @@ def test_c2_full_size_all_distinct():
     assert int(n_out.item()) == n == 1_000_000
     assert bool((cnt == 1).all())
     assert torch.equal(out[: n * 32], fl[: n * 32])  # every row is its own first-seen row, input order kept
+
+
+def test_tied_first_seen_offsets_resolve_to_the_lowest_row():
+    """Rows that share the first-seen offset (the same table twice, i.e. each record listed twice;
+    tables of two captures merged, both starting at offset 24): one output row per flow, the
+    lowest tied row, counts summed (every tied row was marked first)."""
+    blob = synth.flow_mix(30_000, n_flows=700, seed=21)
+    fl, f6, n = device_table(blob)
+    twice = torch.cat([fl[: n * 32], fl[: n * 32]]).contiguous()
+    twice6 = torch.cat([f6[: n * 32], f6[: n * 32]]).contiguous()
+    _, _, cnt, k = check(twice, twice6, 2 * n)
+    single = device.dev_flow_aggregate(fl, f6, n=n)
+    torch.cuda.synchronize()
+    assert k == int(single[3].item())
+    assert bool((cnt[:k] % 2 == 0).all())
+    # two different captures merged: their first records both sit at offset 24
+    blob2 = synth.flow_mix(20_000, n_flows=300, seed=22)
+    fl2, f62, n2 = device_table(blob2)
+    cat = torch.cat([fl[: n * 32], fl2[: n2 * 32]]).contiguous()
+    cat6 = torch.cat([f6[: n * 32], f62[: n2 * 32]]).contiguous()
+    check(cat, cat6, n + n2)
+
+
+def test_row_cap_is_rejected():
+    fl = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(Exception):
+        device.dev_flow_aggregate(fl, None, n=(1 << 30) + 1, cap=0)

@@ -121,3 +121,51 @@ def test_dev_convert_c2_full_size():
     recs = records_of(blob)
     assert check_convert(blob, recs) == 1_000_000
     check_dense(blob, recs)
+
+
+def dev_details(blob, recs):
+    import ctypes
+    import net_parser_rs as npr
+    ctx = npr.context(0)
+    n = len(recs)
+    buf, r = dev(np.frombuffer(blob, np.uint8)), dev(recs)
+    st = torch.zeros(max(n, 1), dtype=torch.uint8, device="cuda")
+    det = torch.zeros(max(n, 1), dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream()
+    ctx.check(ctx.lib.npr_dev_flow_details(ctx.handle, buf.data_ptr(), buf.numel(), r.data_ptr(), n, st.data_ptr(),
+                                           det.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    torch.cuda.synchronize()
+    return st[:n].cpu().numpy(), det[:n].cpu().numpy().view(np.uint64)
+
+
+@pytest.mark.parametrize("name", sorted(CORPORA) + ["vxlan", "flow_mix"])
+def test_flow_error_details_match_oracle(name):
+    """The payload each record's error variant carries (include/npr.h npr_flow_details: Needed sizes,
+    remainders, failure offsets, versions, EtherTypes, protocol ids), device vs oracle, on parsed and
+    shrunk+permuted record lists (shrinking produces every Incomplete step)."""
+    blob = {"vxlan": lambda: synth.vxlan_corpus(3_000), "flow_mix": lambda: synth.flow_mix(5_000)}.get(
+        name, CORPORA.get(name))()
+    for recs in (records_of(blob), records_of(blob, shrink=0.5, permute=True, seed=9)):
+        want_st, want_det = _oracle.flow_details(blob, recs)
+        st, det = dev_details(blob, recs)
+        assert np.array_equal(st, want_st)
+        assert np.array_equal(det, want_det)
+
+
+def test_flow_error_details_host_call_and_mirror():
+    """npr_flow_details (host memory) and the mirror's FlowError.size / .detail."""
+    import net_parser_rs as npr
+    from net_parser_rs import flow
+    blob = synth.quirk_corpus(2_000, seed=13)
+    rem, f = npr.CaptureFile.parse(blob)
+    recs = f.records.into_inner()
+    want_st, want_det = _oracle.flow_details(blob, records_of(blob))
+    st, det = flow._details(recs[0]._buf, recs)
+    assert np.array_equal(st, want_st) and np.array_equal(det, want_det)
+    seen = 0
+    for i in np.nonzero(want_st != 0)[0][:40]:
+        with pytest.raises(flow.FlowError) as e:
+            recs[i].extract_flow()
+        assert e.value.code == want_st[i] and e.value.detail == int(want_det[i])
+        seen += e.value.size is not None
+    assert seen > 0

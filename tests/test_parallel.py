@@ -270,3 +270,91 @@ def test_gloo_world2_device_step_protocol(wrong, pipelined):
     flows_ok, v6_ok, rounds = q.get(timeout=10)
     assert flows_ok and v6_ok
     assert (rounds > 1) == wrong
+
+
+# ---- side rows when the root holds no flows; a record spanning a whole shard -------
+def _v6_gather_main(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob = synth.quirk_corpus(3_000, seed=38)
+        _, _, recs, _ = _oracle.capture_file_parse(blob)
+        flows, v6 = _oracle.convert_records(blob, recs)
+        assert ((flows["kind"] & _abi.KIND_IPV6) != 0).any()
+        # rank 0 (the root) holds no Ok flow; rank 1 holds every flow, IPv6 ones included
+        metas = [parallel.ShardResult(24, 24, 0, 0), parallel.ShardResult(24, len(blob), len(recs), len(flows))]
+        empty = parallel.ShardResult(24, 24, 0, 0, np.zeros(0, _abi.FLOW_DTYPE), np.zeros(0, _abi.FLOW_V6_DTYPE))
+        full = parallel.ShardResult(24, len(blob), len(recs), len(flows), flows, v6)
+        got = parallel.gather_flows(empty if rank == 0 else full, metas, [True, True])
+        if rank == 0:
+            m, m6 = got
+            q.put((m.tobytes() == flows.tobytes(), m6 is not None and v6_rows(m, m6) == v6_rows(flows, v6)))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_v6_rows_root_without_flows():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_v6_gather_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    flows_ok, v6_ok = q.get(timeout=10)
+    assert flows_ok and v6_ok
+
+
+def spanning_capture():
+    """64-B records, then ONE record whose payload spans the middle third of the capture, then more
+    64-B records: with three equal byte ranges, no record starts in rank 1's range."""
+    import struct
+    a = synth.fixed64(150)
+    b = synth.fixed64(150, seed=77, with_header=False)
+    jumbo = struct.pack("<IIII", 1_600_000_000, 999_999, 30_000, 30_000) + bytes(30_000)
+    return a + jumbo + b
+
+
+def _span_rank_main(rank, world, port, blob, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hdr, recs, cons, flows, v6 = full_reference(blob, with_v6=True)
+        bounds = parallel.shard_bounds(24, len(blob), world)
+        lo, hi = bounds[rank]
+        base = 0 if rank == 0 else lo - lo % 16
+        shard = torch.from_numpy(np.frombuffer(blob[base:], dtype=np.uint8).copy())
+        # rank 1's speculation finds no record start (there is none): its first byte is the guess
+        ws = OracleShardWorkspace(len(recs) + 1, spec_exact(recs))
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
+        metas, live, rounds = step.step()
+        fl, f6 = step.rows()
+        merged, _ = parallel.gather_flow_tables(fl, None, metas, live)
+        if rank == 0:
+            q.put((merged.numpy().tobytes() == flows.tobytes(), metas[1].n_records, rounds))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world3_record_spans_a_whole_shard():
+    blob = spanning_capture()
+    bounds = parallel.shard_bounds(24, len(blob), 3)
+    _, recs, _, _ = full_reference(blob)
+    offs = recs["offset"]
+    assert not ((offs >= bounds[1][0]) & (offs < bounds[1][1])).any()  # no record starts in rank 1's range
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_span_rank_main, args=(r, 3, port, blob, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    flows_ok, n1, rounds = q.get(timeout=10)
+    assert flows_ok and n1 == 0 and rounds == 2
