@@ -15,7 +15,11 @@
  *   - Status codes 1..3 map 1:1 onto crate::errors::Error (src/errors.rs:3-11);
  *     negative codes are boundary errors the Rust API cannot produce.
  *   - A context is per host thread (the Rust functions are pure and reentrant; a context
- *     owns one device, one stream and its workspaces, so give each thread its own).
+ *     owns one device, one stream and its workspaces, so give each thread its own).  Any number
+ *     of contexts may launch on one device at once: libnpr orders their parse launches (whose
+ *     workgroups wait for one another) so that two never interleave on the CUs.  A stream passed
+ *     to a call must stay valid until the next call on that device from another stream (or a
+ *     device synchronisation): the order is recorded on it lazily.
  */
 #ifndef NPR_H
 #define NPR_H
@@ -236,12 +240,8 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   again in one go.  Off by default: from pageable host memory the chunked copies measured
  *   slower than one copy, and the copy is ~50x the parse, so overlap gains little.
  * NPR_OPT_PARK_FLOWS: accepted for ABI 2 callers, no effect.
- * NPR_OPT_PIPE (default 0; env NPR_PIPE=1 sets 1 at create): 1 makes the resident flows-only pass the
- *   pipelined one (tiles dealt round-robin to the persistent waves, each round's convert_records
- *   rows written while later rounds stream; one launch for any capture size); 0 runs the
- *   contiguous-range resident pass (one grid-wide prefix, then all rows; chained launches above
- *   ~100 MB; the default while the pipelined pass measures slower).  Same results
- *   either way.
+ * NPR_OPT_PIPE: the pipelined resident pass was an experiment that measured slower
+ *   and is not in this library: 0 is accepted, 1 returns NPR_ERR_ARG.
  * NPR_OPT_DEVICE_WINDOW (chunks, default 0 = auto): npr_parse_extract_pipelined keeps at most N
  *   chunks of the capture (a ring, plus a 260 KiB halo for records that straddle a chunk end) and
  *   3 links' flow rows on the device, so a host capture larger than device memory streams through
@@ -380,6 +380,24 @@ typedef struct npr_shard {
 npr_status npr_dev_parse_extract_shard(npr_ctx *ctx, const void *input, uint64_t input_len,
                                        npr_endianness endianness, const npr_shard *shard,
                                        const npr_dev_outputs *out, void *stream);
+/* Several independent device-resident captures (e.g. consecutive capture batches of a stream) in ONE
+ * resident launch: each item is what npr_dev_parse_extract(ctx, input, len, start, endianness, &out,
+ * stream) would parse, with the same outputs and summary (check each with npr_dev_check).  The
+ * workgroups take the captures in order, and each capture's prefix resolution and row writes overlap
+ * the read of the next capture's first bytes; the launch's ramp and tail are paid
+ * once.  Items that need more than flows (record table, offsets, status) or that one launch does not
+ * hold run as their own npr_dev_parse_extract, in order. */
+typedef struct npr_batch_item {
+  const void *input;
+  uint64_t len;
+  uint64_t start;
+  int32_t endianness; /* npr_endianness */
+  int32_t reserved;
+  npr_dev_outputs out;
+} npr_batch_item;
+
+npr_status npr_dev_parse_extract_batch(npr_ctx *ctx, const npr_batch_item *items, uint32_t n, void *stream);
+
 /* Synchronise `stream`, copy the summary back and map its flags to a status. */
 npr_status npr_dev_check(npr_ctx *ctx, const npr_dev_outputs *out, void *stream,
                          npr_summary *host_summary);

@@ -39,13 +39,11 @@ struct npr_ctx {
   DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
   int resident = 1;        // NPR_OPT_RESIDENT
   uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
-  uint32_t pipe_waves = 0; // ... of the pipelined resident pass (a multiple of 15)
   bool res_pack = false;   // chained(): its links pack sparse tiles into kept rounds
-  int pipe = 0;            // NPR_OPT_PIPE: 1 = flows-only launches run k_parse_pipe (0: k_parse_resident)
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
-  const npr_summary *sum_ptr[2] = {nullptr, nullptr};  // summaries the last two launches wrote
-  uint32_t sum_epoch[2] = {0, 0};
-  uint32_t sum_next = 0;
+  // which launch (epoch) wrote which summary, newest last: npr_dev_check checks a summary against
+  // the launch that wrote it, a chained launch the epoch of the one that wrote its `prev`
+  std::vector<std::pair<const npr_summary *, uint32_t>> sum_log;
   // staging for the host-memory entry points
   DevBuf in, recs, status, flows, flows_v6, flows2, flows2_v6, agg;
   // host flows-only parses: the capture's H2D copy in chunks on copy_stream, each chunk's chained
@@ -138,8 +136,6 @@ npr_status res_geometry(npr_ctx *c) {
   HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const int per = npr::resident_waves_per_cu();
   c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
-  const int pper = npr::pipe_waves_per_cu();  // parser waves (15 per workgroup)
-  c->pipe_waves = (uint32_t)std::max<int>((int)npr::kPipeGroupTiles, cus * pper);
   return NPR_OK;
 }
 
@@ -168,35 +164,58 @@ constexpr int kMaxDevices = 64;
 struct DeviceOrder {
   std::mutex m;
   hipEvent_t ev[kOrderEvents] = {};
-  int cur = -1;  // the event behind the last ordered launch (-1: none yet)
+  int cur = -1;                     // the event behind the last ordered launch (-1: none yet)
+  hipStream_t last = nullptr;       // the stream of the last ordered launch
+  bool pending = false;             // mode 3: that launch has no event yet
 };
 DeviceOrder &device_order(int dev) {
   static DeviceOrder orders[kMaxDevices];
   return orders[dev & (kMaxDevices - 1)];
 }
-bool launch_order_enabled() {  // (NPR_LAUNCH_ORDER=0: off, for A/B timing of the event cost only)
-  static const bool on = [] {
+// How the order is kept (NPR_LAUNCH_ORDER, for A/B timing only; measured on C2, µs per launch):
+//   3 (default): a launch records no event; the next launch from ANOTHER stream first records one
+//     on the previous launch's stream, then waits for it (30.0, as with no ordering at all);
+//   1: every launch waits for the previous launch's event and records its own (33.0: an event
+//     record between two launches costs ~2.7 us of GPU time); 2: the wait only across streams
+//     (33.0); 0: no ordering (30.0; two contexts' launches may deadlock).
+int launch_order_mode() {
+  static const int mode = [] {
     const char *e = getenv("NPR_LAUNCH_ORDER");
-    return !(e && e[0] == '0');
+    return e && e[0] >= '0' && e[0] <= '3' ? e[0] - '0' : 3;
   }();
-  return on;
+  return mode;
+}
+npr_status order_record(npr_ctx *c, DeviceOrder &o, hipStream_t s) {
+  const int k = (o.cur + 1) % kOrderEvents;
+  if (!o.ev[k]) HIP_CHECK(c, hipEventCreateWithFlags(&o.ev[k], hipEventDisableTiming));
+  HIP_CHECK(c, hipEventRecord(o.ev[k], s));
+  o.cur = k;
+  return NPR_OK;
 }
 // Run `launch` (enqueues one look-back kernel on s) after every earlier look-back launch on this
 // device; the device's order lock is held from the wait to the record.
 template <class F>
 npr_status ordered_launch(npr_ctx *c, hipStream_t s, F &&launch) {
-  if (!launch_order_enabled()) {
+  const int mode = launch_order_mode();
+  if (mode == 0) {
     HIP_CHECK(c, launch());
     return NPR_OK;
   }
   DeviceOrder &o = device_order(c->device);
   std::lock_guard<std::mutex> g(o.m);
-  if (o.cur >= 0) HIP_CHECK(c, hipStreamWaitEvent(s, o.ev[o.cur], 0));
+  npr_status st;
+  if (mode == 3 && o.pending && o.last != s) {  // the previous launch's event, recorded only now
+    if ((st = order_record(c, o, o.last))) return st;
+    o.pending = false;
+  }
+  if (o.cur >= 0 && (mode == 1 || o.last != s)) HIP_CHECK(c, hipStreamWaitEvent(s, o.ev[o.cur], 0));
   HIP_CHECK(c, launch());
-  const int k = (o.cur + 1) % kOrderEvents;
-  if (!o.ev[k]) HIP_CHECK(c, hipEventCreateWithFlags(&o.ev[k], hipEventDisableTiming));
-  HIP_CHECK(c, hipEventRecord(o.ev[k], s));
-  o.cur = k;
+  o.last = s;
+  if (mode == 3) {
+    o.pending = true;
+  } else if ((st = order_record(c, o, s))) {
+    return st;
+  }
   return NPR_OK;
 }
 
@@ -221,8 +240,7 @@ static uint64_t group_slots(uint64_t nt) {
   uint64_t folds = 0;
   for (int l = 1; l <= npr::kLevels; ++l) folds += n[l];
   const uint64_t res = (std::min<uint64_t>(nt, npr::kResMaxWaves) + npr::kResWgMin - 1) / npr::kResWgMin;
-  const uint64_t pipe = (nt + npr::kPipeGroupTiles - 1) / npr::kPipeGroupTiles;  // k_parse_pipe: one per 15 tiles
-  return std::max(std::max(folds, res), pipe);
+  return std::max(folds, res);
 }
 // tile slots, then the group slots: one allocation (granules are epoch-tagged, so the layout may
 // shift between launches)
@@ -249,8 +267,6 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   }
   const char *env = getenv("NPR_RESIDENT");
   if (env && env[0] == '0') c->resident = 0;
-  const char *penv = getenv("NPR_PIPE");
-  if (penv && penv[0]) c->pipe = penv[0] != '0';
   *out = c;
   return NPR_OK;
 }
@@ -259,6 +275,14 @@ void npr_ctx_destroy(npr_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  {  // the launch order must not record on this context's stream after it is gone (its work is done)
+    DeviceOrder &o = device_order(c->device);
+    std::lock_guard<std::mutex> g(o.m);
+    if (o.last == c->stream) {
+      o.last = nullptr;
+      o.pending = false;
+    }
+  }
   for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->chain, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
                     &c->flows2_v6, &c->agg})
     if (b->p) (void)hipFree(b->p);
@@ -291,10 +315,9 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
       if (value < 0) return fail(c, NPR_ERR_ARG, "NPR_OPT_RESIDENT must be >= 0");
       c->resident = value;
       return NPR_OK;
-    case NPR_OPT_PIPE:  // 1: flows-only launches run the pipelined resident pass (default 0)
-      if (value < 0 || value > 1) return fail(c, NPR_ERR_ARG, "NPR_OPT_PIPE must be 0 or 1");
-      c->pipe = value;
-      return NPR_OK;
+    case NPR_OPT_PIPE:  // the pipelined pass was an experiment: not in this library
+      if (value == 0) return NPR_OK;
+      return fail(c, NPR_ERR_ARG, "NPR_OPT_PIPE: the pipelined resident pass is not built into this library");
     case NPR_OPT_DEVICE_WINDOW:  // chunks of the capture on the device at once (0 = auto)
       if (value < 0 || value == 1 || value == 2) return fail(c, NPR_ERR_ARG, "NPR_OPT_DEVICE_WINDOW: 0 (auto) or >= 3 chunks");
       c->window = value;
@@ -384,7 +407,7 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness e, const npr_dev_outputs *o, void *stream) {
   // flows-only captures larger than one launch keeps in registers: chained chunks of that size
-  if (c && o && c->resident && !c->pipe && !o->record_offsets && !o->records && !o->record_status && len > start) {
+  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start) {
     npr_status st = res_geometry(c);
     if (st) return st;
     if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
@@ -406,6 +429,16 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
                                npr_endianness e, int speculative_start, uint64_t ref_record,
                                const npr_summary *prev, const npr_dev_outputs *o, void *stream,
                                const ShardSpec *sh = nullptr);
+// the epoch of the last launch that wrote summary s (0: none of ours)
+static uint32_t summary_epoch(const npr_ctx *c, const npr_summary *s) {
+  for (auto it = c->sum_log.rbegin(); it != c->sum_log.rend(); ++it)
+    if (it->first == s) return it->second;
+  return 0;
+}
+static void log_summary(npr_ctx *c, const npr_summary *s) {
+  if (c->sum_log.size() >= 256) c->sum_log.erase(c->sum_log.begin(), c->sum_log.begin() + 128);
+  c->sum_log.emplace_back(s, c->epoch);
+}
 static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
                           npr_endianness e, int speculative_start, uint64_t ref_record, const npr_dev_outputs *o,
                           uint64_t chunk_bytes, void *stream, const ShardSpec *sh);
@@ -602,29 +635,9 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.prev_epoch = 0;  // the epoch of the launch that wrote *prev, when it was one of ours: the
     // most recent of the last two launches that wrote that address (an older launch may have
     // used the same summary slot)
-    for (uint32_t k = 0; k < 2; ++k) {
-      const uint32_t i = c->sum_next ^ 1u ^ k;
-      if (c->sum_ptr[i] == prev) {
-        p.prev_epoch = c->sum_epoch[i];
-        break;
-      }
-    }
+    p.prev_epoch = summary_epoch(c, prev);
   }
-  if (resident && c->pipe) {  // the pipelined pass: whole workgroups of 15 parsers, tiles dealt round-robin
-    if ((st = res_geometry(c))) return st;
-    const uint64_t G = npr::kPipeGroupTiles;
-    uint64_t wv = std::min<uint64_t>(nt, c->pipe_waves);
-    if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
-    wv = std::min<uint64_t>((wv + G - 1) / G * G, c->pipe_waves / G * G);
-    p.nwaves = (uint32_t)wv;
-    p.pipe = 1;
-    p.rslots = (npr::RangeSlot *)c->slots.p;  // one per tile
-    p.rgroups = p.groups[1];                  // G(q, b) at q * workgroups + b: one per 15 tiles
-    const uint64_t ng = (nt + npr::kPipeGroupTiles - 1) / npr::kPipeGroupTiles;
-    if ((const char *)(p.rgroups + ng) > (const char *)c->slots.p + c->slots.cap)
-      return fail(c, NPR_ERR_ARG, "internal: pipelined group slots exceed the workspace (%llu groups)",
-                  (unsigned long long)ng);
-  } else if (resident) {
+  if (resident) {
     if ((st = res_geometry(c))) return st;
     uint64_t wv = std::min<uint64_t>(nt, c->res_waves);
     if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
@@ -640,9 +653,7 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
   }
   if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_extract(p, s); }))) return st;
-  c->sum_ptr[c->sum_next] = o->summary;  // who wrote which summary (chained launches check it)
-  c->sum_epoch[c->sum_next] = c->epoch;
-  c->sum_next ^= 1u;
+  log_summary(c, o->summary);  // who wrote which summary (npr_dev_check, chained launches check it)
   return NPR_OK;
 }
 
@@ -652,10 +663,85 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   HIP_CHECK(c, hipMemcpyAsync(c->summary_h, o->summary, sizeof(npr_summary), hipMemcpyDeviceToHost, s));
   HIP_CHECK(c, hipStreamSynchronize(s));
   if (hs) *hs = *c->summary_h;
-  if (c->summary_h->epoch != c->epoch) {
+  const uint32_t want = summary_epoch(c, o->summary);  // the launch that wrote this summary
+  if (c->summary_h->epoch != (want ? want : c->epoch)) {
     return fail(c, NPR_ERR_TIMEOUT, "parse did not complete (tile hand-off timed out)");
   }
   if (c->summary_h->flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded (flags=%u)", c->summary_h->flags);
+  return NPR_OK;
+}
+
+// ---- K independent captures in one resident launch (k_parse_batch) ------------------------------
+// Eligible: flows-only outputs, the resident pass on, a capture one launch keeps in registers
+// (npr_dev_parse_extract would not chain it).  Anything else runs item by item.
+static bool batch_eligible(npr_ctx *c, const npr_batch_item &it) {
+  const npr_dev_outputs &o = it.out;
+  if (!c->resident || o.record_offsets || o.records || o.record_status || !o.summary) return false;
+  if (!it.input || it.len <= it.start || ((uintptr_t)it.input & 15u)) return false;
+  if (o.flows && (((uintptr_t)o.flows & 15u) || (o.flows_v6 && ((uintptr_t)o.flows_v6 & 15u)))) return false;
+  if (it.len >= (1ull << 40)) return false;
+  return it.len - it.start <= (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
+}
+
+static npr_status batch_group(npr_ctx *c, const npr_batch_item *items, uint32_t n, hipStream_t s) {
+  npr::BatchParams bp{};
+  bp.n = n;
+  uint64_t off[npr::kMaxBatch + 1] = {0};
+  uint64_t nts[npr::kMaxBatch];
+  for (uint32_t k = 0; k < n; ++k) {  // slot regions: each capture's range slots, then its workgroup slots
+    npr::ParseParams &p = bp.p[k];
+    const npr_batch_item &it = items[k];
+    npr_status st = range_params(c, it.input, it.len, it.start, it.len, (npr_endianness)it.endianness, 0, it.start,
+                                 nullptr, p, nts[k]);
+    if (st) return st;
+    uint64_t wv = std::min<uint64_t>(nts[k], c->res_waves);
+    if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
+    p.nwaves = (uint32_t)wv;
+    const uint64_t nb = (wv + npr::kResWgMin - 1) / npr::kResWgMin;
+    off[k + 1] = off[k] + wv * sizeof(npr::RangeSlot) + nb * sizeof(npr::GroupSlot);
+  }
+  npr_status st = ensure(c, c->slots, off[n], true);
+  if (st) return st;
+  if ((st = next_epoch(c, s))) return st;  // one epoch for the launch: an abort stops every capture
+  for (uint32_t k = 0; k < n; ++k) {
+    npr::ParseParams &p = bp.p[k];
+    const npr_dev_outputs &o = items[k].out;
+    char *region = (char *)c->slots.p + off[k];
+    p.epoch = c->epoch;
+    p.timeout_ticks = kTimeoutTicks;
+    p.rslots = (npr::RangeSlot *)region;
+    p.rgroups = (npr::GroupSlot *)(region + (uint64_t)p.nwaves * sizeof(npr::RangeSlot));
+    p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
+    p.abort_word = c->abort_word;
+    p.flows = (uint32_t *)o.flows;
+    p.flows_v6 = (uint32_t *)o.flows_v6;
+    p.flow_cap = o.flow_cap;
+    p.summary = o.summary;
+  }
+  if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_batch(bp, s); }))) return st;
+  for (uint32_t k = 0; k < n; ++k) log_summary(c, items[k].out.summary);
+  return NPR_OK;
+}
+
+npr_status npr_dev_parse_extract_batch(npr_ctx *c, const npr_batch_item *items, uint32_t n, void *stream) {
+  if (!c || (!items && n)) return fail(c, NPR_ERR_ARG, "null argument");
+  HIP_CHECK(c, hipSetDevice(c->device));
+  npr_status st = res_geometry(c);
+  if (st) return st;
+  hipStream_t s = pick(c, stream);
+  for (uint32_t i = 0; i < n;) {
+    uint32_t k = 0;
+    while (k < npr::kMaxBatch && i + k < n && batch_eligible(c, items[i + k])) ++k;
+    if (k >= 2) {
+      if ((st = batch_group(c, items + i, k, s))) return st;
+      i += k;
+    } else {  // one capture (or one that a single launch does not hold): the ordinary call
+      const npr_batch_item &it = items[i];
+      if ((st = npr_dev_parse_extract(c, it.input, it.len, it.start, (npr_endianness)it.endianness, &it.out, stream)))
+        return st;
+      ++i;
+    }
+  }
   return NPR_OK;
 }
 

@@ -45,7 +45,7 @@ struct alignas(128) GroupSlot {
 // a = the range's speculative aggregate {exit, entry + 1, cnt, ok} (phase A); p = the exact
 // inclusive prefix through the range {exit, cnt, ok} (phase B).  Each workgroup folds its waves'
 // aggregates into one GroupSlot (g) and looks back over the lower workgroups' G (decoupled
-// look-back); e is unused by the resident pass.  The pipelined pass uses one slot per TILE.
+// look-back); e is unused by the resident pass.
 struct alignas(128) RangeSlot {
   uint64_t a[4];
   uint64_t p[3];
@@ -121,25 +121,27 @@ struct ParseParams {
   uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][kStampWords] or NULL
   // resident single pass (flows-only launches): 0 = use the two-pass kernels
   uint32_t nwaves;         // persistent waves, each owning a contiguous tile range (<= kResMaxWaves, <= ntiles)
-  RangeSlot *rslots;       // [nwaves] (pipe: [ntiles])
-  GroupSlot *rgroups;      // workgroup aggregates G(b), [ceil(nwaves / kResWg)] (pipe: [rounds * workgroups])
+  RangeSlot *rslots;       // [nwaves]
+  GroupSlot *rgroups;      // workgroup aggregates G(b), [ceil(nwaves / kResWg)]
   uint32_t *rcnt;          // pacing counter word (res_arrive; never read)
-  uint32_t pipe;           // 1: the pipelined resident pass (k_parse_pipe): nwaves = parser waves (15 per
-                           //    workgroup), tile t = round * nwaves + parser, rslots[t] per TILE,
-                           //    rgroups[t / 15] per workgroup round
   uint32_t pack;           // resident pass: sparse tiles share kept rounds (k_parse_resident<.., true>)
   const npr_summary *prev; // chained launch (resident pass only): continue the chain and the counts
   uint32_t prev_epoch;     //   of the launch that wrote *prev (its epoch, 0 = unchecked); NULL = none
 };
 
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)
-// k_parse_resident, one launch of p.nwaves persistent waves in 16-wave workgroups (p.pipe:
-// k_parse_pipe, 15 parser waves + 1 resolver per workgroup).
+// k_parse_resident, one launch of p.nwaves persistent waves in 16-wave workgroups.
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
-// resident waves per CU the hardware admits for k_parse_resident / k_parse_pipe (occupancy query)
+// k_parse_batch: bp.n independent flows-only captures (each p[k] a resident launch's parameters,
+// its own slot region and summary, one shared epoch) in one launch of max nwaves waves
+constexpr uint32_t kMaxBatch = 8;
+struct BatchParams {
+  uint32_t n;
+  ParseParams p[kMaxBatch];
+};
+hipError_t launch_parse_batch(const BatchParams &bp, hipStream_t s);
+// resident waves per CU the hardware admits for k_parse_resident (occupancy query)
 int resident_waves_per_cu();
-int pipe_waves_per_cu();
-constexpr uint32_t kPipeGroupTiles = 15;  // tiles per group slot of the pipelined pass (its parser waves per workgroup)
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);

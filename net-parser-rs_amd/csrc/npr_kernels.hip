@@ -24,17 +24,15 @@
 //   k_parse_resident (flows-only launches, the default): persistent waves, each owning a
 //     contiguous tile range, flows kept in registers; one pass with a decoupled look-back over
 //     16-wave workgroup aggregates (chained launches for captures past what registers hold);
-//   k_parse_pipe (flows-only launches, opt-in NPR_OPT_PIPE / NPR_PIPE=1; measured slower):
-//     persistent workgroups of 15 parser waves + 1
-//     resolver wave; tiles are dealt round-robin (tile = round * parsers + parser), so every
-//     round is a contiguous slab of the capture; the resolver folds each round's aggregates and
-//     posts every parser's exact prefix while the parsers stream on (npr_kernels_pipe.inc).
+//   k_parse_batch: several independent captures in one resident launch, each capture's look-back
+//     and row writes overlapping the read of the next one's first tiles.
 // A wrong speculation costs a wait or a re-walk, never a wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <type_traits>
 
+#include "npr_decode.hpp"  // decode<>: the general per-record decode tree (host + device)
 #include "npr_internal.hpp"
 
 namespace npr {
@@ -48,7 +46,6 @@ constexpr uint32_t kInclMax = 1u << 18;   // speculation: plausible incl_len bou
 // ---------------------------------------------------------------------------------------------
 // byte access
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t be16_of(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0xffu); }
 
 // 4 bytes at LDS byte address a (any alignment) as a little-endian u32: two aligned dword reads
 // (merged into ds_read2_b32) + v_alignbyte.
@@ -102,204 +99,6 @@ struct GlobalReader {
   }
 };
 
-// ---------------------------------------------------------------------------------------------
-// per-record decode: FlowExtraction::extract_flow (src/flow/mod.rs:23-41) as one straight-line
-// function.  Returns an npr_flow_status; with FIELDS it also fills the 32-B npr_flow words
-// (d[0..6]; the record offset goes in by the caller) and the IPv6 addresses.
-// Length checks are ordered exactly like the reference's do_parse! steps so the FIRST failing
-// step decides between Incomplete / Failure / Custom.
-// ---------------------------------------------------------------------------------------------
-struct FlowWords {
-  uint32_t d[7];
-  uint32_t v6[8];
-  uint32_t v6off;  // payload offset of the IPv6 address block (the resident kernel re-reads it)
-  uint32_t l4off;  // payload offset of the L4 header (decode<> only; the VXLAN path reads past it)
-};
-
-// InternetProtocolId::new (src/layer3/mod.rs:54-72)
-__device__ __forceinline__ bool proto_known(uint32_t v) {
-  return v == 0 || v == 1 || v == 6 || v == 17 || v == 43 || v == 44 || v == 50 || v == 51 ||
-         v == 59 || v == 60;
-}
-// InternetProtocolId::has_next_option (src/layer3/mod.rs:74-84)
-__device__ __forceinline__ bool proto_has_next(uint32_t v) {
-  return v == 0 || v == 43 || v == 44 || v == 50 || v == 51 || v == 60;
-}
-
-// DETAIL (the error-payload kernel only; compiled out everywhere else): *det = the payload the
-// reference's error variant carries for the returned status (include/npr.h npr_flow_detail):
-//   Incomplete of a nom primitive -> its Needed::Size (nom 4: the primitive's full size, take!(k) -> k)
-//   a remainder left after a layer  -> rem.len()        (src/flow/layer2/ethernet.rs:67-76 ...)
-//   map_opt! / map_res! failures    -> the frame offsets [start, end) of the failing primitive's input
-//                                      (nom's error position and its parser's input end): start | end << 32
-//   version != 4 / 6                -> the version nibble (the Custom message's value)
-//   LLDP / 802.3 length             -> the EtherType;  IP protocol not TCP/UDP -> the protocol id
-// Primitive sizes of the fixed headers, in parse order (the first one that does not fit is the
-// Incomplete one):
-__constant__ const uint8_t kNeedIpv4[10] = {1, 1, 2, 2, 2, 1, 1, 2, 4, 4};  // src/layer3/ipv4.rs:96-122
-__constant__ const uint8_t kNeedIpv6[4] = {1, 3, 2, 1};                     // src/layer3/ipv6.rs:58-66, :90
-__constant__ const uint8_t kNeedIpv6Tail[3] = {1, 16, 16};                  // src/layer3/ipv6.rs:41-43
-__constant__ const uint8_t kNeedArp[9] = {2, 2, 1, 1, 2, 6, 4, 6, 4};       // src/layer3/arp.rs:55-64
-__constant__ const uint8_t kNeedTcp[8] = {2, 2, 4, 4, 2, 2, 2, 2};          // src/layer4/tcp.rs:64-86
-__constant__ const uint8_t kNeedUdp[4] = {2, 2, 2, 2};                      // src/layer4/udp.rs:38-41
-__device__ __forceinline__ uint64_t first_short(const uint8_t *sizes, int cnt, uint64_t avail) {
-  uint64_t end = 0;
-  for (int i = 0; i < cnt; ++i) {
-    end += sizes[i];
-    if (end > avail) return sizes[i];
-  }
-  return 0;
-}
-template <bool DETAIL>
-__device__ __forceinline__ uint32_t fail(uint64_t *det, uint32_t code, uint64_t v) {
-  if (DETAIL) *det = v;
-  return code;
-}
-
-template <bool FIELDS, class R, bool DETAIL = false>
-__device__ __forceinline__ uint32_t decode(const R &r, uint32_t n, FlowWords &f, uint64_t *det = nullptr) {
-  if (DETAIL) *det = 0;
-  // ---- Ethernet::parse (src/layer2/ethernet.rs:204-216): two mac_address (take!(6))
-  if (n < 12) return fail<DETAIL>(det, NPR_FLOW_ETH_INCOMPLETE, 6);
-  uint32_t m0 = 0, m1 = 0, m2 = 0;
-  if (FIELDS) {
-    m0 = r.le32(0);  // dst[0..3]
-    m1 = r.le32(4);  // dst[4..5] src[0..1]
-    m2 = r.le32(8);  // src[2..5]
-  }
-  // parse_vlan_tag recursion (:163-202): map_opt!(be_u16, EthernetTypeId::new), 802.1Q/ad tags
-  uint32_t pos = 12, vlan = 0, etype;
-  bool tagged = false;
-  for (;;) {
-    if (n - pos < 2) return fail<DETAIL>(det, NPR_FLOW_ETH_INCOMPLETE, 2);
-    const uint32_t w = r.le32(pos);
-    const uint32_t t = be16_of(w);
-    if (t != 0x8100u && t != 0x88a8u) {
-      // EthernetTypeId::new (:57-73): LLDP / IPv4 / IPv6 / ARP / <=1500 (length), else None
-      if (!(t == 0x88ccu || t == 0x0800u || t == 0x86ddu || t == 0x0806u || t <= 1500u))
-        return fail<DETAIL>(det, NPR_FLOW_ETH_FAILURE, pos | ((uint64_t)n << 32));
-      etype = t;
-      pos += 2;
-      break;
-    }
-    if (n - pos - 2 < 2) return fail<DETAIL>(det, NPR_FLOW_ETH_INCOMPLETE, 2);  // TCI: be_u16 (:176)
-    if (!tagged) vlan = be16_of(w >> 16) & 0x0FFFu;                             // vlans_to_vlan: first tag (:134-137)
-    tagged = true;
-    pos += 4;
-  }
-  // ---- layer-3 dispatch (src/flow/layer2/ethernet.rs:55-131); payload = rest
-  const uint32_t l3 = pos, n3 = n - pos;
-  uint32_t l4, n4, proto;
-  bool v6;
-  if (etype == 0x0800u) {
-    // IPv4::parse (src/layer3/ipv4.rs:148-160) -> parse_ipv4 (:76-146)
-    if (n3 < 1) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, 1);
-    const uint32_t w0 = r.le32(l3);
-    const uint32_t b0 = w0 & 0xffu;
-    if ((b0 >> 4) != 4u) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_CUSTOM, b0 >> 4);
-    const uint32_t hw = b0 & 0x0Fu, hl = hw * 4u, add = hw > 5u ? (hw - 5u) * 4u : 0u;
-    if (n3 < 4) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, DETAIL ? first_short(kNeedIpv4, 10, n3) : 0);  // tos, length
-    const uint32_t length = (be16_of(w0 >> 16) - hl) & 0xffffu;  // u16 wrapping (:100)
-    const uint64_t expected = (uint64_t)hl + add + length;        // (:107)
-    if (n3 < 10) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, DETAIL ? first_short(kNeedIpv4, 10, n3) : 0);
-    proto = (r.le32(l3 + 8) >> 8) & 0xffu;
-    if (!proto_known(proto)) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_FAILURE, (l3 + 9u) | ((uint64_t)n << 32));  // map_opt! (:119)
-    if (n3 < 20) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, DETAIL ? first_short(kNeedIpv4, 10, n3) : 0);
-    if (n3 - 20u < length) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, length);  // payload: take!(length)
-    uint64_t p4 = 20ull + length;
-    if (add) {                                                // options (:124)
-      if ((uint64_t)n3 - p4 < add) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, add);
-      p4 += add;
-    }
-    if ((uint64_t)n3 > expected) {                            // padding (:125-129)
-      const uint64_t pad = (uint64_t)n3 - expected;
-      if ((uint64_t)n3 - p4 < pad) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_INCOMPLETE, pad);
-      p4 += pad;
-    }
-    if (p4 != n3) return fail<DETAIL>(det, NPR_FLOW_L2_IPV4_REMAINDER, (uint64_t)n3 - p4);  // rem.is_empty() (:67-76)
-    if (FIELDS) {
-      f.d[0] = r.le32(l3 + 12);
-      f.d[1] = r.le32(l3 + 16);
-    }
-    l4 = l3 + 20u;  // the L4 parse starts right after the fixed header (quirk Q7)
-    n4 = length;
-    v6 = false;
-  } else if (etype == 0x86ddu) {
-    // IPv6::parse (src/layer3/ipv6.rs:87-99) -> parse_ipv6 (:58-71) -> parse_next_header (:29-56)
-    if (n3 < 1) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_INCOMPLETE, 1);
-    if ((r.u8(l3) >> 4) != 6u) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_CUSTOM, r.u8(l3) >> 4);
-    if (n3 < 7) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_INCOMPLETE, DETAIL ? first_short(kNeedIpv6, 4, n3) : 0);  // take!(3), be_u16, be_u8
-    const uint32_t w1 = r.le32(l3 + 4);
-    const uint32_t plen = be16_of(w1);
-    uint32_t nh = (w1 >> 16) & 0xffu;
-    if (!proto_known(nh)) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_FAILURE, (l3 + 6u) | ((uint64_t)n << 32));
-    uint32_t p = 7;
-    while (proto_has_next(nh)) {                              // one byte per extension (quirk Q11)
-      if (n3 - p < 1) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_INCOMPLETE, 1);
-      nh = r.u8(l3 + p);
-      if (!proto_known(nh)) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_FAILURE, (l3 + p) | ((uint64_t)n << 32));
-      ++p;
-    }
-    if (n3 - p < 33u)                                          // hop limit, src, dst
-      return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_INCOMPLETE, DETAIL ? first_short(kNeedIpv6Tail, 3, n3 - p) : 0);
-    const uint32_t sa = l3 + p + 1u;
-    p += 33u;
-    if (n3 - p < plen) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_INCOMPLETE, plen);  // payload: take!(p)
-    if (n3 - p != plen) return fail<DETAIL>(det, NPR_FLOW_L2_IPV6_REMAINDER, n3 - p - plen);
-    if (FIELDS) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) f.v6[k] = r.le32(sa + 4u * (uint32_t)k);
-      f.v6off = sa;
-      f.d[0] = 0;
-      f.d[1] = 0;
-    }
-    l4 = l3 + p;
-    n4 = plen;
-    proto = nh;
-    v6 = true;
-  } else if (etype == 0x0806u) {
-    // Arp::parse: 28 fixed bytes (src/layer3/arp.rs:54-76); the flow is always Err
-    if (n3 < 28) return fail<DETAIL>(det, NPR_FLOW_L2_ARP_INCOMPLETE, DETAIL ? first_short(kNeedArp, 9, n3) : 0);
-    if (n3 != 28) return fail<DETAIL>(det, NPR_FLOW_L2_ARP_REMAINDER, n3 - 28u);
-    return NPR_FLOW_L3_ARP;
-  } else {
-    return fail<DETAIL>(det, NPR_FLOW_L2_ETHERTYPE, etype);  // LLDP / PayloadLength (:125-130)
-  }
-  // ---- layer-4 dispatch (src/flow/layer3/ipv4.rs:49-101, ipv6.rs:49-100)
-  bool udp;
-  if (proto == 6u) {
-    // Tcp::parse (src/layer4/tcp.rs:59-101)
-    const uint32_t inc = v6 ? NPR_FLOW_L3_IPV6_TCP_INCOMPLETE : NPR_FLOW_L3_IPV4_TCP_INCOMPLETE;
-    if (n4 < 14) return fail<DETAIL>(det, inc, DETAIL ? first_short(kNeedTcp, 8, n4) : 0);
-    const uint32_t thl = (be16_of(r.le32(l4 + 12)) >> 12) * 4u;  // extract_length (:54-57)
-    if (thl < 20u || thl > 60u)  // map_res! (:68): the error's position is the be_u16's input
-      return fail<DETAIL>(det, v6 ? NPR_FLOW_L3_IPV6_TCP_FAILURE : NPR_FLOW_L3_IPV4_TCP_FAILURE,
-                         (l4 + 12u) | ((uint64_t)(l4 + n4) << 32));
-    if (n4 < thl) return fail<DETAIL>(det, inc, DETAIL ? (n4 < 20u ? first_short(kNeedTcp, 8, n4) : thl - 20u) : 0);
-    udp = false;  // payload: rest -> never a remainder
-  } else if (proto == 17u) {
-    // Udp::parse (src/layer4/udp.rs:33-50): take!(length - 8) with usize wrapping
-    const uint32_t inc = v6 ? NPR_FLOW_L3_IPV6_UDP_INCOMPLETE : NPR_FLOW_L3_IPV4_UDP_INCOMPLETE;
-    if (n4 < 8) return fail<DETAIL>(det, inc, DETAIL ? first_short(kNeedUdp, 4, n4) : 0);
-    const uint32_t L = be16_of(r.le32(l4 + 4));
-    if (L < 8u || n4 - 8u < L - 8u) return fail<DETAIL>(det, inc, (uint64_t)L - 8ull);  // (usize wrap below 8)
-    if (n4 != L)
-      return fail<DETAIL>(det, v6 ? NPR_FLOW_L3_IPV6_UDP_REMAINDER : NPR_FLOW_L3_IPV4_UDP_REMAINDER, n4 - L);
-    udp = true;
-  } else {
-    return fail<DETAIL>(det, v6 ? NPR_FLOW_L3_IPV6_PROTOCOL : NPR_FLOW_L3_IPV4_PROTOCOL, proto);
-  }
-  if (FIELDS) {  // Flow::new (src/flow/mod.rs:64-86)
-    f.l4off = l4;
-    const uint32_t wp = r.le32(l4);
-    f.d[2] = be16_of(wp) | (be16_of(wp >> 16) << 16);
-    f.d[3] = vlan | (m1 & 0xffff0000u);
-    f.d[4] = m2;
-    f.d[5] = m0;
-    f.d[6] = (m1 & 0xffffu) | (((v6 ? NPR_FLOW_KIND_IPV6 : 0u) | (udp ? NPR_FLOW_KIND_UDP : 0u)) << 16);
-  }
-  return NPR_FLOW_OK;
-}
 
 // ---------------------------------------------------------------------------------------------
 // fast decode: Ethernet (untagged) / IPv4 (IHL 5) or IPv6 (no extension) / TCP or UDP.
@@ -933,7 +732,6 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) {  // byte address i
 template <bool BIG>
 __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, uint32_t r, uint32_t incl,
                                             uint32_t hop_span, uint32_t &n, uint32_t &last) {
-#ifndef NPR_HOP_CXX
   // The loop by hand (the compiled one spent ~17 SALU per hop on flow blocks and copies): per hop
   // one broadcast ds_write_b16 of the offset, two ds_read_b32 of the next header's incl_len word
   // pair, v_alignbyte + readfirstlane, and three compare-and-branch exits; the srec address walks
@@ -976,23 +774,6 @@ __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, u
   else NPR_HOP_ASM("");
 #undef NPR_HOP_ASM
   return r;
-#else
-  for (;;) {
-    srec[n] = (uint16_t)r;
-    ++n;
-    r += incl + 16u;
-    last = incl;
-    if (r >= hop_span) break;
-    incl = incl_at<BIG>(w, r);
-    uint32_t d;  // incl, or kTile + 1 when it repeats the last length: one compare to leave on
-    asm("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %1"
-        : "=s"(d)
-        : "s"(incl), "s"(__builtin_amdgcn_readfirstlane(last)), "s"((uint32_t)kTile + 1u)
-        : "scc");  // (readfirstlane: an "s" operand the allocator had put in a VGPR fails to assemble)
-    if (d > (uint32_t)kTile) break;
-  }
-  return r;
-#endif
 }
 
 __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
@@ -1247,25 +1028,14 @@ __global__ __launch_bounds__(kWave) void k_count_tiles(ParseParams kp) {
   if (!known) {
     const SpecCtx sc = spec_ctx(kp, scb);
     const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
-#ifdef NPR_EXP_NOSPEC  // ablation (C2 only): the exact entry of the fixed 80-B stride
-    entry = tile_lo + (uint32_t)((80u - (uint32_t)((tile_lo - 24u) % 80u)) % 80u);
-    (void)sc;
-#else
     entry = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
-#endif
     if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
   }
   entry = uni64(entry);
   if (DIAG) stamp_at(st, 8);
   uint32_t n = 0;
   uint64_t ex = entry == kNone ? 0ull : entry;
-#ifdef NPR_EXP_NOWALK  // ablation (C2 only)
-  n = (uint32_t)((tile_hi - entry + 79) / 80);
-  ex = entry + 80ull * n;
-  sh.srec[lane] = (uint16_t)(entry - tile_lo + 80u * lane);
-#else
   if (entry != kNone && entry >= tile_lo && entry < tile_hi) ex = walk_tile(kp, w, sh.srec, tile_lo, tile_hi, entry, n);
-#endif
   ex = uni64(ex);
   wave_sync();
   if (DIAG) stamp_at(st, 9);
@@ -1282,12 +1052,7 @@ __global__ __launch_bounds__(kWave) void k_count_tiles(ParseParams kp) {
   if (DIAG) stamp_at(st, 10);
   // Ok count: status-only decode of every record
   uint32_t okc = 0;
-#ifdef NPR_EXP_NOCOUNT  // ablation (C2 only)
-  okc = n;
-  for (int s = 0; s < 0; ++s) {
-#else
   for (int s = 0; s < kRounds; ++s) {
-#endif
     if ((uint32_t)s * 64u >= n) break;
     const uint32_t i = lane + (uint32_t)s * 64u;
     const bool valid = i < n;  // every lane decodes (stale offsets are in-bounds), masked after
@@ -1546,25 +1311,7 @@ __device__ __forceinline__ uint32_t res_wave_of(const ParseParams &kp, int64_t m
   const uint64_t big = (uint64_t)r * (q + 1);
   return (uint64_t)m < big ? (uint32_t)((uint64_t)m / (q + 1)) : (uint32_t)(r + ((uint64_t)m - big) / q);
 }
-// L2 prefetch beyond the LDS ring: one LDS-DMA of a dword from every 128-B line of the tile into
-// a junk LDS word per lane (an LDS destination, so no VGPR is written behind the compiler's back;
-// bytes past the range are out of the descriptor and fetch nothing).  The ring's DMA of the tile,
-// kPfAhead iterations later, then hits the XCD's L2 instead of waiting out an HBM round trip: a
-// sparse capture's tile is walked in far less time than that latency.
-#ifndef NPR_PF_AHEAD
-#define NPR_PF_AHEAD 0
-#endif
-constexpr int kPfAhead = NPR_PF_AHEAD;  // tiles prefetched beyond the ring (0, the default: measured slower at C2 and C3)
 constexpr uint32_t kStepPrioTiles = 8;  // wave ranges up to this many tiles use stepped priorities
-constexpr int kPfAfter = kPfAhead ? (kResRing < kPfAhead + 1 ? kResRing : kPfAhead + 1) : 0;  // PFs after any DMA
-__device__ __forceinline__ void pf_tile(const ParseParams &kp, uint64_t tile_lo, uint64_t hi, uint32_t *junk) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t avail = hi > tile_lo ? hi - tile_lo : 0;
-  const uint32_t nbytes = avail < (uint64_t)kTile ? (uint32_t)avail : (uint32_t)kTile;
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + (avail ? tile_lo : 0)), 0, (int)nbytes, 0x00020000);
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lds_ptr_t)junk, 4, lane * 128u, 0, 0, 0);
-}
 // wait until at most `ahead` tiles' DMAs are outstanding (the youngest vector-memory
 // instructions are the DMAs of the tiles ahead and at least PF prefetches, so this retires the
 // current tile)
@@ -1602,11 +1349,7 @@ __device__ __forceinline__ bool res_sentinel(const ParseParams &kp, uint64_t *p,
 // hand-off granule read: a returning atomic (the coherent value even when this XCD's L2 holds a
 // line from an earlier poll)
 __device__ __forceinline__ uint64_t ld_res(uint64_t *p) {
-#ifdef NPR_RES_PLAIN_POLL
-  return ld_agent(p);
-#else
   return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 // one lane's element of a window: lvl 0 = wave v's A, lvl 1 = workgroup b's aggregate G(b)
 __device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr, bool sc1 = false) {
@@ -1796,13 +1539,7 @@ __device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t
 
 // 16-B flow-row store.  Plain (write-back): measured 33.9 us per launch against 38.1 us with
 // write-through (sc1) stores, although the table is written in the launch's last microseconds.
-__device__ __forceinline__ void st_wt16(uint32_t *p, u32x4 v) {
-#ifdef NPR_EXP_WT_FLOW_STORES
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#else
-  *reinterpret_cast<u32x4 *>(p) = v;
-#endif
-}
+__device__ __forceinline__ void st_wt16(uint32_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
 
 // one Ok flow row (+ its IPv6 side row, re-read from the capture at the decoded offset)
 __device__ __forceinline__ void res_put_v6(const ParseParams &kp, uint64_t o, const uint32_t (&s)[8], uint64_t p);
@@ -1887,22 +1624,64 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
 
 struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS fold
   ResShared w[kResWg];
-  uint32_t junk[64];  // L2-prefetch destinations (every wave's, overwritten freely)
   uint32_t prog[kResWg];  // tiles each wave has parsed in phase A (~0: done or inactive), for fair priorities
   Seg a[kResWg];   // each wave's range aggregate A
   Seg x[kResWg];   // each wave's prefix: anchor ⊕ G(0..b-1) ⊕ A(waves before it here)
   uint32_t fail;   // a bounded wait of wave 0 timed out: every wave leaves
 };
 
-// PACK: sparse tiles share kept rounds (links sized past one round per tile; the host sets it from
-// the capture's density).  A separate instantiation: the merge costs dense captures registers.
-template <bool DIAG, bool PACK>
-__global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ResWgShared sh;
+// What staging a capture's first tiles needs of its parameters (res_stage), passed by value: the
+// batch kernel reads them from its kernel arguments as scalars.
+struct StageParams {
+  const uint8_t *buf;
+  uint64_t len, org, ref;
+  uint32_t ntiles, nwaves, flags;
+};
+__device__ __forceinline__ StageParams stage_params(const ParseParams &kp) {
+  return StageParams{kp.buf, kp.len, kp.org, kp.ref, kp.ntiles, kp.nwaves, kp.flags};
+}
+
+// The first n tiles of wave v's range in a capture into its LDS ring (slots 0..n-1), behind the
+// capture's speculation-context bytes (issued first, so they land with the first tile).  Returns
+// those bytes (spec_ctx_load's).
+__device__ __forceinline__ uint32_t res_stage(const StageParams &q, ResShared &w, uint32_t v, uint32_t n) {
+  ParseParams kp{};  // the fields dma_tile / spec_ctx_load / res_range read
+  kp.buf = q.buf;
+  kp.len = q.len;
+  kp.org = q.org;
+  kp.ref = q.ref;
+  kp.ntiles = q.ntiles;
+  kp.nwaves = q.nwaves;
+  kp.flags = q.flags;
+  uint32_t c0 = 0, c1 = 0;
+  if (v < kp.nwaves) res_range(kp, v, c0, c1);
+  const uint32_t scb = spec_ctx_load(kp);
+  const uint64_t base = kp.org + (uint64_t)c0 * kTile;
+#pragma unroll
+  for (int k = 0; k < kResRing; ++k)
+    if ((uint32_t)k < n && c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, w.data[k]);
+  return scb;
+}
+
+// One capture of the resident pass (the kernel comment above).  Run by every wave of the workgroup.
+//   BATCH (k_parse_batch): one capture of several in the launch.  nx is the following capture
+//   (kn == bp->n: none): while this workgroup's prefix is being resolved, each wave stages the first
+//   kResRing tiles of its range of the next capture in its idle ring (the read that the look-back and the
+//   row writes would otherwise leave HBM without), so `next` starts with them landed; `staged`
+//   says this capture's tiles were staged that way, with its speculation bytes in scb.  The rows
+//   go out one per lane (the ring slot the single-capture pass stages row blocks in holds the next capture).
+// Returns false when the workgroup must leave the kernel (a bounded wait timed out).
+template <bool DIAG, bool PACK, bool BATCH>
+__device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &sh, bool has_next, StageParams nx,
+                                            bool staged, uint32_t &scb) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar LDS bases
   const uint32_t b = blockIdx.x, v = b * kResWg + wid;
   const uint32_t nb = (kp.nwaves + kResWg - 1) / kResWg;
+  if (BATCH && b >= nb) {  // no range of this capture here (a smaller capture): stage the next one
+    if (has_next) scb = res_stage(nx, sh.w[wid], v, kResRing);
+    return true;
+  }
   const uint32_t nw = kp.nwaves - b * kResWg < kResWg ? kp.nwaves - b * kResWg : kResWg;  // waves of this workgroup
   const bool active = wid < nw;
   Stamps st;
@@ -1911,18 +1690,14 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   if (active) res_range(kp, v, c0, c1);
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
   const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;  // chained: tile 0 speculates too
-  if (threadIdx.x == 0) sh.fail = 0;
   if (lane == 0) sh.prog[wid] = active && c0 < c1 ? 0u : ~0u;
-  const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
+  if (!staged) {
+    scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
 #pragma unroll
-  for (int k = 0; k < kResRing - 1; ++k)
-    if (c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
-  const uint64_t range_end = kp.org + (uint64_t)c1 * kTile < kp.len ? kp.org + (uint64_t)c1 * kTile : kp.len;
-#pragma unroll
-  for (int k = 0; k < kPfAhead; ++k) pf_tile(kp, base + (uint64_t)(kResRing - 1 + k) * kTile, range_end, sh.junk);
-#ifndef NPR_EXP_NOPRIO
+    for (int k = 0; k < kResRing - 1; ++k)
+      if (c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
+  }
   __builtin_amdgcn_s_setprio(3);  // lowered by one per tile parsed (below)
-#endif
 
   // ---- phase A ------------------------------------------------------------------------------
   uint32_t fl[kResSlots][8];                   // kept rounds: d[0..6] (IPv6: d[0] = address offset), record offset - base
@@ -1943,11 +1718,16 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     const uint32_t k = t - c0, slot = k % kResRing;
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    if (t + kResRing - 1 < c1)
+    // (staged: tiles 0 .. kResRing-1 are already in flight)
+    if (t + kResRing - 1 < c1 && (!staged || k >= 1u))
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
-    if (kPfAhead) pf_tile(kp, tile_lo + (uint64_t)(kResRing - 1 + kPfAhead) * kTile, range_end, sh.junk);
     const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    res_wait<kPfAfter>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    if (staged && k == 0u) {  // the staged tiles and the previous capture's row stores: all of them
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      wave_sync();
+    } else {
+      res_wait<0>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
+    }
     if (DIAG) wait_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
     if (t == c0) {
       sc = spec_ctx(kp, scb);
@@ -1992,12 +1772,7 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
             const bool valid = pack ? (lane >= fu && lane < fu + n) : i < n;
             FlowWords f;
             const uint32_t rel = sh.w[wid].srec[i];
-#ifdef NPR_EXP_NODECODE  // ablation (timing only: wrong flow fields)
-            f = FlowWords{};
-            const bool okr = valid;
-#else
             const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
-#endif
             const uint64_t bal = __ballot(okr);
             const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
                                     f.d[4], f.d[5], f.d[6], (uint32_t)(tile_lo + rel - base)};
@@ -2031,7 +1806,6 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       }
     }
     wave_sync();  // done with this slot before it is refilled
-#ifndef NPR_EXP_NOPRIO
     // keep the CU's waves in step: the SIMD arbiter favours older waves, which would finish their
     // ranges long before the younger ones (C3: the four age ranks of a SIMD finished phase A at
     // 125 / 139 / 157 / 179 us), and the workgroup waits for its last.  Long ranges: each tile, a
@@ -2053,11 +1827,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       else if (d == 2) __builtin_amdgcn_s_setprio(1);
       else __builtin_amdgcn_s_setprio(0);
     }
-#endif
   }
-#ifndef NPR_EXP_NOPRIO
   if (lane == 0) sh.prog[wid] = ~0u;  // done: no longer the slowest
-#endif
   if (DIAG) stamp_at(st, 2);
   const uint32_t ep = kp.epoch;
   if (active && lane == 0) {  // A: in LDS for the workgroup fold, in HBM for the rare generic prefix
@@ -2079,6 +1850,8 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
+  // waves 2..15 stage the next capture's first tiles now (0 and 1 hold wave 0's kept flows below)
+  if (has_next && wid >= 2u) scb = res_stage(nx, sh.w[wid], v, kResRing);
   if (wid == 0) {
     // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
     // flows wait there, so the windows get the registers.
@@ -2118,68 +1891,54 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     if (DIAG) stamp_at(st, 12);
     Seg E = start_seg(kp);
     uint64_t entry0 = kp.start;
-    if (okw) {
-      LaneSeg G[kTopWin];
+    LaneSeg G[kTopWin];
 #pragma unroll
-      for (int w = 0; w < kTopWin; ++w) {  // descending inside a window (fold_window's order)
-        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-        G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
-      }
-      // every window at once: re-read (returning atomics) only the aggregates not yet this
-      // launch's -- not published yet, or a line an earlier launch left in this XCD's L2
-      uint32_t nap = 1;
-      for (int tries = 0;; ++tries) {
-        bool miss = false;
-#pragma unroll
-        for (int w = 0; w < kTopWin; ++w) {
-          const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-          miss = miss || __ballot((uint32_t)lane < sz && !G[w].present) != 0ull;
-        }
-        if (!miss) break;
-        if (tries && !res_nap(kp, t0, nap)) {
-          okw = false;
-          break;
-        }
-#pragma unroll
-        for (int w = 0; w < kTopWin; ++w) {
-          const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-          const bool need = (uint32_t)lane < sz && !G[w].present;
-          if (__ballot(need)) {
-            const LaneSeg N = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, need);
-            if (need) G[w] = N;
-          }
-        }
-      }
-      if (DIAG) stamp_at(st, 13);
-      if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
-        const uint64_t pc = kp.prev->consumed, pr = kp.prev->n_records, pf = kp.prev->n_flows;
-        okw = okw && (kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch);  // it completed
-        entry0 = kp.prev->entry;  // the chain's first record, as the first link reported it
-        E.entry = E.exit = pc;
-        E.cnt = pr;
-        E.ok = pf;
-      } else if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
-        entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
-        E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
-      }
-#ifdef NPR_EXP_NOFOLD  // ablation (timing only, C2's fixed 80-B records): E from G(b-1)'s exit, no fold
-      if (b > 0 && okw) {
-        uint64_t ex = 0;
-#pragma unroll
-        for (int w = 0; w < kTopWin; ++w)
-          if (64u * (uint32_t)w < b) ex = rl64(G[w].exit, 0);
-        E.exit = ex;
-        E.cnt = E.ok = (ex - kp.start) / 80u;  // exact for C2's 80-B records only: rows land where they belong
-        E.last = sh.a[0].first - 1;
-      }
-#else
+    for (int w = 0; w < kTopWin; ++w) {  // descending inside a window (fold_window's order)
+      const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+      G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
+    }
+    // every window at once: re-read (returning atomics) only the aggregates not yet this
+    // launch's -- not published yet, or a line an earlier launch left in this XCD's L2
+    uint32_t nap = 1;
+    for (int tries = 0;; ++tries) {
+      bool miss = false;
 #pragma unroll
       for (int w = 0; w < kTopWin; ++w) {
-        const uint32_t w0 = 64u * (uint32_t)w;
-        if (w0 >= b || !okw) break;
-        E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
+        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+        miss = miss || __ballot((uint32_t)lane < sz && !G[w].present) != 0ull;
       }
-#endif
+      if (!miss) break;
+      if (tries && !res_nap(kp, t0, nap)) {
+        okw = false;
+        break;
+      }
+#pragma unroll
+      for (int w = 0; w < kTopWin; ++w) {
+        const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+        const bool need = (uint32_t)lane < sz && !G[w].present;
+        if (__ballot(need)) {
+          const LaneSeg N = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, need);
+          if (need) G[w] = N;
+        }
+      }
+    }
+    if (DIAG) stamp_at(st, 13);
+    if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
+      const uint64_t pc = kp.prev->consumed, pr = kp.prev->n_records, pf = kp.prev->n_flows;
+      okw = okw && (kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch);  // it completed
+      entry0 = kp.prev->entry;  // the chain's first record, as the first link reported it
+      E.entry = E.exit = pc;
+      E.cnt = pr;
+      E.ok = pf;
+    } else if (kp.flags & kFlagSpecStart) {  // anchor: the entry wave 0 speculated
+      entry0 = b == 0 ? sh.a[0].entry : rl64(G[0].entry, (int)(b < 64u ? b : 64u) - 1);
+      E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
+    }
+#pragma unroll
+    for (int w = 0; w < kTopWin; ++w) {
+      const uint32_t w0 = 64u * (uint32_t)w;
+      if (w0 >= b || !okw) break;
+      E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
     }
     if (DIAG) stamp_at(st, 14);
     // (3) each wave's prefix
@@ -2195,15 +1954,29 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
       for (int j = 0; j < 8; ++j) fl[q][j] = stash[(q * 8 + j) * 64 + lane];
   }
   __syncthreads();
-  if (!active || sh.fail) return;
+  if (sh.fail) return false;
+  // waves 0 and 1: their rings are free again
+  if (has_next && wid < 2u) scb = res_stage(nx, sh.w[wid], v, kResRing);
+  if (!active) return true;
 
   // ---- phase B ------------------------------------------------------------------------------
   Seg X = sh.x[wid];
-  if (!X.valid && !res_prefix(kp, v, X, t0)) return;
+  if (!X.valid && !res_prefix(kp, v, X, t0)) return false;
   if (DIAG) stamp_at(st, 4);
   const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1 - 1);
   uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
   const bool before_end = X.exit < tile_end(kp, X.last);  // the chain ended before this range
+  // the ring re-read paths (deferred tiles, a mis-speculated range) need the ring: the staged tiles
+  // of `next` land first and are staged again afterwards
+  auto ring_take = [&]() {
+    if (has_next) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      wave_sync();
+    }
+  };
+  auto ring_give = [&]() {
+    if (has_next) scb = res_stage(nx, sh.w[wid], v, kResRing);
+  };
   if (!before_end && xe < range_hi && xe >= range_lo) {
     if (entry != kNone && xe == entry) {  // the speculated chain is the exact one: flows from registers
       if (kp.flows) {
@@ -2213,17 +1986,16 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
             const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
             const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
                                  (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
-#ifndef NPR_ROWS_PER_LANE
             // The round's Ok rows are one contiguous block of nok rows: stage them in this wave's idle
             // ring slot in address order, then store the block as contiguous 16-B chunks (lane i:
-            // chunks i and 64 + i), so each store instruction writes whole lines.  A write-only
-            // microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane rounds
-            // (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s
-            // (4.2-5.7 drained); in this kernel C2 went 31.3 -> 30.8 us (NPR_ROWS_PER_LANE: the
-            // per-lane stores).
+            // chunks i and 64 + i), so each store instruction writes whole lines, non-temporally.  A
+            // write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane
+            // rounds (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s;
+            // in this kernel C2 went 31.3 -> 30.8 us, and non-temporal stores a further 30.6 -> 30.1.
+            // (BATCH: the ring holds the next capture's tiles: one row per lane.)
             const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
             const uint64_t f0 = xo + okb;
-            if (nok && f0 + nok <= kp.flow_cap) {
+            if (!BATCH && nok && f0 + nok <= kp.flow_cap) {
               const bool mine = (bal >> lane) & 1ull;
               const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
               const uint64_t p = base + fl[q][7];
@@ -2236,42 +2008,32 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
               }
               wave_sync();
               u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
-#ifndef NPR_ROWS_WB  // non-temporal (streaming) stores: 30.1 vs 30.6 us at C2 with write-back ones
               if ((uint32_t)lane < 2u * nok) __builtin_nontemporal_store(stg[lane], dst + lane);
               if ((uint32_t)lane + 64u < 2u * nok) __builtin_nontemporal_store(stg[lane + 64], dst + lane + 64);
-#else
-              if ((uint32_t)lane < 2u * nok) dst[lane] = stg[lane];
-              if ((uint32_t)lane + 64u < 2u * nok) dst[lane + 64] = stg[lane + 64];
-#endif
               if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
-#ifdef NPR_ROWS_DRAIN  // (drained rounds measured 31.2 vs 30.8 us undrained at C2, 30.9 vs 30.6 again)
-              __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-#endif
               wave_sync();  // the slot is rewritten by the next round
             } else if ((bal >> lane) & 1ull) {
               const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
               if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
             }
-#else
-            if ((bal >> lane) & 1ull) {
-              const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-              if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
-            }
-#endif
           }
         }
       }
       if (DIAG) stamp_at(st, 5);
       if (tdef < c1) {
         uint64_t dc = xc + cdef, dok = xo + odef;
+        ring_take();
         (void)res_emit(kp, sh.w[wid], tdef, c1, pdef, dc, dok);
+        ring_give();
         if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - tdef);
       }
       xe = pos;
       xc += cnt;
       xo += okc;
     } else {  // mis-speculated: re-read the whole range from the exact position
+      ring_take();
       xe = uni64(res_emit(kp, sh.w[wid], c0, c1, xe, xc, xo));
+      ring_give();
       if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - c0);
     }
   }
@@ -2300,23 +2062,38 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams k
     st.v[7] = walk_ticks;
     stamp_flush(kp, st, v, wid == 0 ? 0xFFFFu : 0x8FFFu);
   }
+  return true;
 }
 
-#ifndef NPR_NO_PIPE  // (experiment builds whose tile geometry the pipelined pass does not fit)
-#include "npr_kernels_pipe.inc"
-#endif
-
-int pipe_waves_per_cu() {
-#ifdef NPR_NO_PIPE
-  return 0;
-#else
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_pipe<false>), kPipeWg * kWave, 0) !=
-      hipSuccess)
-    return 0;
-  return nb * (int)kPipePar;  // parser waves
-#endif
+// PACK: sparse tiles share kept rounds (links sized past one round per tile; the host sets it from
+// the capture's density).  A separate instantiation: the merge costs dense captures registers.
+template <bool DIAG, bool PACK>
+__global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams kp) {
+  __shared__ __attribute__((aligned(16))) ResWgShared sh;
+  uint32_t scb = 0;
+  (void)res_capture<DIAG, PACK, false>(kp, sh, false, StageParams{}, false, scb);
 }
+
+// =============================================================================================
+// BATCHED RESIDENT PASS — k_parse_batch: bp.n independent captures (each one resident launch's
+// worth, flows-only) in ONE launch.  The workgroups run the captures in order; capture k's
+// look-back and row writes overlap the read of capture k+1's first tiles (res_capture BATCH), and
+// the launch's own ramp and tail are paid once for the batch.  Every capture has its own slot
+// region and summary; all share the launch's epoch (so one abort stops them all).  A workgroup
+// only ever waits for LOWER workgroups of the same capture, which never wait for it: workgroups
+// drifting apart across captures cannot deadlock.
+// =============================================================================================
+template <bool PACK>
+__global__ __launch_bounds__(kResWg * kWave) void k_parse_batch(BatchParams bp) {
+  __shared__ __attribute__((aligned(16))) ResWgShared sh;
+  uint32_t scb = 0;
+  for (uint32_t k = 0; k < bp.n; ++k) {
+    const bool has_next = k + 1 < bp.n;
+    const StageParams nx = has_next ? stage_params(bp.p[k + 1]) : StageParams{};
+    if (!res_capture<false, PACK, true>(bp.p[k], sh, has_next, nx, k > 0, scb)) return;
+  }
+}
+
 
 int resident_waves_per_cu() {
   int nb = 0;
@@ -2336,14 +2113,6 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
 }
 
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
-#ifndef NPR_NO_PIPE
-  if (p.nwaves && p.pipe) {
-    const uint32_t nb = p.nwaves / kPipePar;
-    if (p.stats || p.stamps) hipLaunchKernelGGL((k_parse_pipe<true>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
-    else hipLaunchKernelGGL((k_parse_pipe<false>), dim3(nb), dim3(kPipeWg * kWave), 0, s, p);
-    return hipGetLastError();
-  }
-#endif
   if (p.nwaves) {
     const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
     const bool diag = p.stats || p.stamps;
@@ -2353,6 +2122,15 @@ hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
     return hipGetLastError();
   }
   return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
+}
+
+hipError_t launch_parse_batch(const BatchParams &bp, hipStream_t s) {
+  uint32_t waves = 0;
+  for (uint32_t k = 0; k < bp.n; ++k) waves = bp.p[k].nwaves > waves ? bp.p[k].nwaves : waves;
+  if (bp.n == 0 || bp.n > kMaxBatch || waves == 0) return hipErrorInvalidValue;
+  const uint32_t nb = (waves + kResWg - 1) / kResWg;
+  hipLaunchKernelGGL(k_parse_batch<false>, dim3(nb), dim3(kResWg * kWave), 0, s, bp);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2594,14 +2372,15 @@ __global__ __launch_bounds__(kBlock) void k_flow_detail(const uint8_t *buf, uint
   const npr_record rc = load_record(recs, i);
   const uint64_t off = rc.offset + 16;
   uint32_t st = 0xffu;  // the record does not lie inside the buffer
-  uint64_t d = 0;
+  volatile uint64_t scratch_d = 0;
+  volatile uint64_t *dp = detail ? detail + i : &scratch_d;  // decode stores the payload here
+  *dp = 0;
   if (off <= len && len - off >= rc.actual_length) {
     const GlobalReader r{buf + off, len - off};
     FlowWords f;
-    st = decode<false, GlobalReader, true>(r, rc.actual_length, f, &d);
+    st = decode<false, GlobalReader, true>(r, rc.actual_length, f, dp);
   }
   if (status) status[i] = (uint8_t)st;
-  if (detail) detail[i] = d;
 }
 
 hipError_t launch_flow_detail(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n, uint8_t *status,

@@ -41,7 +41,7 @@ VXLAN_PORT = 33
 VXLAN_INCOMPLETE = 34
 VXLAN_INNER = 64  # + the inner frame's npr_flow_status
 VXLAN_PORT_IANA = 4789
-OPT_PIPE = 4  # npr_ctx_set_option: flows-only parses run the pipelined resident pass (1) or the contiguous one (0, default)
+OPT_PIPE = 4  # npr_ctx_set_option: the pipelined pass (an experiment) is not built: only 0 is accepted
 OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's device window in chunks (0 auto, >= 3)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
@@ -82,6 +82,12 @@ class DevOutputsC(ctypes.Structure):
                 ("summary", ctypes.c_void_p)]
 
 
+class BatchItemC(ctypes.Structure):
+    """npr_batch_item: one capture of npr_dev_parse_extract_batch."""
+    _fields_ = [("input", ctypes.c_void_p), ("len", ctypes.c_uint64), ("start", ctypes.c_uint64),
+                ("endianness", ctypes.c_int32), ("reserved", ctypes.c_int32), ("out", DevOutputsC)]
+
+
 class ShardC(ctypes.Structure):
     _fields_ = [("base", ctypes.c_uint64), ("start", ctypes.c_uint64), ("stop", ctypes.c_uint64),
                 ("speculative_start", ctypes.c_int32), ("usec_magic", ctypes.c_int32),
@@ -106,7 +112,7 @@ EXPORTED = [
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
-    "npr_flow_details", "npr_dev_flow_details",
+    "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -165,6 +171,7 @@ _SIGNATURES = {
                                        ctypes.c_int, _vp, _vp, _vp, _vp]),
     "npr_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
     "npr_dev_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
+    "npr_dev_parse_extract_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
 }
 
 _lib = None

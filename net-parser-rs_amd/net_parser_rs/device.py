@@ -131,6 +131,26 @@ class Workspace:
         return self.flows_v6[(self.flow_cap - k) * 32: self.flow_cap * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
 
 
+def launch_batch(items, ctx=None, stream=None):
+    """npr_dev_parse_extract_batch: several captures in ONE resident launch.  items: (ws, buf, start,
+    endianness) per capture, each parsed as ws.launch(buf, start, endianness) would (its outputs in
+    that Workspace; check each with ws.check()).  Asynchronous on `stream` (default: the current
+    stream of the first buffer's device)."""
+    items = list(items)
+    if not items:
+        return
+    ctx = ctx if ctx is not None else items[0][0].ctx
+    s = stream if stream is not None else torch.cuda.current_stream(items[0][1].device)
+    arr = (_abi.BatchItemC * len(items))()
+    for i, (ws, buf, start, e) in enumerate(items):
+        assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
+        arr[i] = _abi.BatchItemC(buf.data_ptr(), buf.numel(), int(start), int(e), 0, ws.outs)
+    ctx.check(ctx.lib.npr_dev_parse_extract_batch(ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(items),
+                                                   ctypes.c_void_p(s.cuda_stream)))
+    for ws, *_ in items:
+        ws._stream = s
+
+
 class Result:
     def __init__(self, ws, sm):
         self.ws = ws

@@ -357,6 +357,11 @@ int or_extract_flow(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow
   return extract_flow_l4(p, n, record_offset, f, v6, NULL, NULL, NULL);
 }
 
+int or_extract_flow_detail(const uint8_t *p, size_t n, uint64_t record_offset, npr_flow *f, npr_flow_v6 *v6,
+                           uint64_t *detail) {
+  return extract_flow_l4(p, n, record_offset, f, v6, NULL, NULL, detail);
+}
+
 /* ---- row f3: src/layer4/vxlan.rs:31-48 (Vxlan::parse) + src/flow/layer4/vxlan.rs:32-50 ----- */
 int or_vxlan_parse(const uint8_t *in, size_t n, int big, or_vxlan *v) {
   size_t pos = 0;

@@ -46,6 +46,9 @@ int or_capture_file_parse(const uint8_t *in, size_t len, npr_global_header *hdr,
  * record_offset is only stored into flow->record_offset. */
 int or_extract_flow(const uint8_t *payload, size_t len, uint64_t record_offset, npr_flow *flow,
                     npr_flow_v6 *v6);
+/* or_extract_flow + the payload its error variant carries (npr.h npr_flow_details) */
+int or_extract_flow_detail(const uint8_t *payload, size_t len, uint64_t record_offset, npr_flow *flow,
+                           npr_flow_v6 *v6, uint64_t *detail);
 /* flow::convert_records: returns the number of flows (writes at most cap). */
 size_t or_convert_records(const uint8_t *buf, size_t len, const npr_record *recs, size_t n,
                           npr_flow *out, npr_flow_v6 *out_v6, size_t cap);

@@ -109,6 +109,13 @@ static void run(npr_ctx *ctx, const char *path) {
   uint8_t *dst_ = calloc(cap, 1);
   or_flow_details(in, len, orec, on, ost, odet);
   CHECK(npr_flow_details(ctx, in, len, orec, on, dst_, det) == NPR_OK, "%s: flow_details", path);
+  for (size_t i = 0, shown = 0; i < on && shown < 5; ++i)
+    if (dst_[i] != ost[i] || det[i] != odet[i]) {
+      fprintf(stderr, "%s: record %zu (offset %llu, len %u): status %u vs %u, detail %llu vs %llu\n", path, i,
+              (unsigned long long)orec[i].offset, orec[i].actual_length, dst_[i], ost[i], (unsigned long long)det[i],
+              (unsigned long long)odet[i]);
+      ++shown;
+    }
   CHECK(!memcmp(dst_, ost, on) && !memcmp(det, odet, on * sizeof *det), "%s: flow error details", path);
   free(det);
   free(odet);

@@ -32,34 +32,8 @@ def to_dev(blob):
     return t[: len(blob)] if blob else t[:0]
 
 
-def check_parity(blob, start=24, endianness=None, ws=None, light=False):
-    """Run the device path on `blob` and compare everything with the oracle.
-
-    light requests flows only (no record table / status), so the flow table, counts and
-    `consumed` are compared.  light=True runs the resident single pass (k_parse_resident, the
-    default for flows-only launches); light=N (an int > 1) the same with at most N waves, so
-    each wave owns a long tile range (kept-round overflow -> deferred tiles, many ranges per
-    64-wave group, speculation at range starts deep inside the capture); light="decode" the
-    two-pass kernels (NPR_OPT_RESIDENT off); light="pipe" / "pipe_wN" the pipelined resident pass
-    (k_parse_pipe, NPR_OPT_PIPE on), the latter with at most N parser waves (many rounds per
-    parser: kept-slot flushes, deferred rounds, the resolver's generic path)."""
-    if isinstance(light, str) and light.startswith("pipe"):
-        ctx = npr.context(0)
-        cap = int(light[6:]) if light.startswith("pipe_w") else 1
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 1))
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, cap))
-        try:
-            return check_parity(blob, start, endianness, ws, light=True)
-        finally:
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 0))
-    if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
-        ctx = npr.context(0)
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
-        try:
-            return check_parity(blob, start, endianness, ws, light=True)
-        finally:
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+def expect(blob, start=24, endianness=None):
+    """The oracle's (records, consumed, flows, flows_v6, status, endianness) of a capture."""
     if start == 24:
         rc, hdr, want_recs, want_cons = _oracle.capture_file_parse(blob)
         assert rc == 0
@@ -72,22 +46,81 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
         want_cons = start + cons
     want_flows, want_v6 = _oracle.convert_records(blob, want_recs)
     _, _, want_status = _oracle.extract_flows(blob, want_recs)
+    return want_recs, want_cons, want_flows, want_v6, want_status, e
+
+
+def check_flows(w, want):
+    """A flows-only workspace's results against expect()'s."""
+    want_recs, want_cons, want_flows, want_v6, _, _ = want
+    sm = w.check()
+    assert sm.n_records == len(want_recs), (sm.n_records, len(want_recs))
+    assert sm.consumed == want_cons, (sm.consumed, want_cons)
+    assert sm.n_flows == len(want_flows)
+    got_flows = w.flows_np()
+    assert got_flows.tobytes() == want_flows.tobytes(), first_diff(got_flows, want_flows)
+    v6mask = (want_flows["kind"] & _abi.KIND_IPV6) != 0
+    if v6mask.any():
+        assert w.flows_v6_np()[v6mask].tobytes() == want_v6[v6mask].tobytes()
+    return sm
+
+
+def check_batch(blob, start=24, endianness=None):
+    """The capture as the middle item of a three-capture npr_dev_parse_extract_batch (k_parse_batch:
+    its first tiles staged during the previous capture's prefix, the next capture's staged during
+    its own), every item against the oracle."""
+    fillers = [synth.fixed64(3_000, seed=77), synth.quirk_corpus(700, seed=78, big=True)]
+    blobs = [fillers[0], blob, fillers[1]]
+    starts = [24, start, 24]
+    wants = [expect(b, s_, endianness if i == 1 else None) for i, (b, s_) in enumerate(zip(blobs, starts))]
+    items = []
+    for b, s_, want in zip(blobs, starts, wants):
+        cap = max((len(b) - s_) // 16 + 1, 1)
+        w = device.Workspace(cap, cap, records=False, status=False)
+        items.append((w, to_dev(b), s_, want[5]))
+    device.launch_batch(items)
+    sms = [check_flows(it[0], want) for it, want in zip(items, wants)]
+    return sms[1]
+
+
+def check_parity(blob, start=24, endianness=None, ws=None, light=False):
+    """Run the device path on `blob` and compare everything with the oracle.
+
+    light requests flows only (no record table / status), so the flow table, counts and
+    `consumed` are compared.  light=True runs the resident single pass (k_parse_resident, the
+    default for flows-only launches); light=N (an int > 1) the same with at most N waves, so
+    each wave owns a long tile range (kept-round overflow -> deferred tiles, many ranges per
+    64-wave group, speculation at range starts deep inside the capture); light="decode" the
+    two-pass kernels (NPR_OPT_RESIDENT off); light="batch" / "batch_wN" the capture inside a batched
+    launch (k_parse_batch), the latter with at most N waves per capture (deferred tiles re-read
+    through a ring that holds the next capture's staged tiles)."""
+    if isinstance(light, str) and light.startswith("batch"):
+        ctx = npr.context(0)
+        cap = int(light[7:]) if light.startswith("batch_w") else 1
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, cap))
+        try:
+            return check_batch(blob, start, endianness)
+        finally:
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+    if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
+        ctx = npr.context(0)
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
+        try:
+            return check_parity(blob, start, endianness, ws, light=True)
+        finally:
+            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+    want = expect(blob, start, endianness)
+    want_recs, want_cons, want_flows, want_v6, want_status, e = want
     buf = to_dev(blob)
     n = len(blob)
     cap = max((n - start) // 16 + 1, 1)
     w = ws or (device.Workspace(cap, cap, records=False, status=False) if light else device.Workspace(cap, cap, status=True))
     w.launch(buf, start=start, endianness=e, nbytes=n)
+    if light:
+        return check_flows(w, want)
     sm = w.check()
     assert sm.n_records == len(want_recs), (sm.n_records, len(want_recs))
     assert sm.consumed == want_cons, (sm.consumed, want_cons)
     assert sm.n_flows == len(want_flows)
-    if light:
-        got_flows = w.flows_np()
-        assert got_flows.tobytes() == want_flows.tobytes(), first_diff(got_flows, want_flows)
-        v6mask = (want_flows["kind"] & _abi.KIND_IPV6) != 0
-        if v6mask.any():
-            assert w.flows_v6_np()[v6mask].tobytes() == want_v6[v6mask].tobytes()
-        return sm
     got_recs = w.records_np()
     assert got_recs.tobytes() == want_recs.tobytes(), first_diff(got_recs, want_recs)
     got_status = w.status_np()
@@ -131,9 +164,9 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, "decode", "pipe", "pipe_w30", "pipe_w150"],
-                                ids=["full", "resident", "resident_w7", "resident_w100", "two_pass", "pipe",
-                                     "pipe_w30", "pipe_w150"])
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, "decode", "batch", "batch_w7", "batch_w100"],
+                                ids=["full", "resident", "resident_w7", "resident_w100", "two_pass", "batch",
+                                     "batch_w7", "batch_w100"])
 
 
 @LIGHT
@@ -386,9 +419,8 @@ def test_capture_past_2GiB():
     del blob
     ctx = npr.context(0)
     try:
-        for resident, pipe in ((1, 0), (1, 1), (0, 0)):
+        for resident in (1, 0):
             ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, resident))
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, pipe))
             w = device.Workspace(n + 1, n + 1, records=False, status=False)
             w.launch(buf, start=24, endianness=hdr.endianness)
             sm = w.check()
@@ -398,4 +430,3 @@ def test_capture_past_2GiB():
             del w
     finally:
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_PIPE, 0))
