@@ -44,6 +44,8 @@ VXLAN_PORT_IANA = 4789
 OPT_PIPE = 4  # npr_ctx_set_option: the pipelined pass (an experiment) is not built: only 0 is accepted
 OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's device window in chunks (0 auto, >= 3)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
+OPT_SEGMENTS = 6  # npr_ctx_set_option: 2 (default) the two-segment resident pass where it applies, 1 never
+PASS_TWO_PASS, PASS_RESIDENT, PASS_SEGMENTED, PASS_BATCH = 1, 2, 3, 4  # npr_ctx_last_pass
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1
 
@@ -105,7 +107,7 @@ assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24 and c
 # Every symbol include/npr.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "npr_version", "npr_abi_version", "npr_ctx_create", "npr_ctx_destroy", "npr_ctx_last_error",
-    "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps", "npr_ctx_set_option",
+    "npr_ctx_set_stats", "npr_ctx_read_stats", "npr_ctx_read_stamps", "npr_ctx_set_option", "npr_ctx_last_pass",
     "npr_workspace_bytes", "npr_global_header_parse", "npr_record_parse", "npr_records_parse",
     "npr_capture_file_parse", "npr_extract_flows", "npr_convert_records", "npr_parse_extract",
     "npr_parse_extract_pipelined", "npr_host_alloc", "npr_host_free",
@@ -128,6 +130,7 @@ _SIGNATURES = {
     "npr_workspace_bytes": (ctypes.c_uint64, [ctypes.c_uint64]),
     "npr_ctx_set_stats": (ctypes.c_int, [_vp, ctypes.c_int]),
     "npr_ctx_set_option": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    "npr_ctx_last_pass": (ctypes.c_int, [_vp]),
     "npr_ctx_read_stats": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int]),
     "npr_ctx_read_stamps": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "npr_global_header_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.POINTER(GlobalHeaderC), _c_size_p]),
