@@ -232,11 +232,6 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   convert_records rows are known.  0 (and every launch that asks for a record table, offsets or
  *   status) runs the two-pass kernels; N > 1 caps the resident pass at N waves (longer ranges per
  *   wave: a test knob).  Same results either way.
- * NPR_OPT_SEGMENTS (default 1; env NPR_SEGS=1|2 sets it at create): 2 = a resident launch whose waves
- *   each get at least two tiles and hold every tile's flows (no packed rounds) runs the two-segment
- *   pass: the capture's halves are parsed one after the other by the same waves, so the first
- *   half's look-back and row writes overlap the second half's parse.  1 runs the
- *   one-segment pass everywhere.  Same results either way.
  * NPR_OPT_STREAM_CHUNK (KiB, default 0 = off): npr_parse_extract without a record table
  *   copies a capture of more than two chunks to the device in chunks on a second stream and
  *   launches each chunk's chained parse as soon as it (and the next chunk) has landed, so the
@@ -257,11 +252,11 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   most 262144 B, which the halo covers).  Windowed chunks are at least 512 KiB.
  */
 enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4,
-       NPR_OPT_DEVICE_WINDOW = 5, NPR_OPT_SEGMENTS = 6 };
+       NPR_OPT_DEVICE_WINDOW = 5 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Which pass the context's last device parse launch ran (tests and diagnostics; no reference
- * counterpart): 0 none yet, 1 the two-pass kernels, 2 the one-segment resident pass, 3 the
- * two-segment resident pass, 4 a batched resident launch. */
+ * counterpart): 0 none yet, 1 the two-pass kernels, 2 the resident single pass, 4 a batched
+ * resident launch. */
 int npr_ctx_last_pass(const npr_ctx *ctx);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

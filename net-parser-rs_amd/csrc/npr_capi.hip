@@ -40,8 +40,6 @@ struct npr_ctx {
   int resident = 1;        // NPR_OPT_RESIDENT
   uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
   bool res_pack = false;   // chained(): its links pack sparse tiles into kept rounds
-  int segs = 1;            // NPR_OPT_SEGMENTS: 2 = the two-segment resident pass where it applies
-  bool seg_ok = false;     // k_parse_seg runs res_waves waves too (occupancy query)
   int last_pass = 0;       // npr_ctx_last_pass
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
   // which launch (epoch) wrote which summary, newest last: npr_dev_check checks a summary against
@@ -139,7 +137,6 @@ npr_status res_geometry(npr_ctx *c) {
   HIP_CHECK(c, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device));
   const int per = npr::resident_waves_per_cu();
   c->res_waves = (uint32_t)std::max(1, std::min<int>((int)npr::kResMaxWaves, cus * per));
-  c->seg_ok = (uint64_t)cus * (uint64_t)npr::seg_waves_per_cu() >= c->res_waves;
   return NPR_OK;
 }
 
@@ -237,15 +234,14 @@ static void level_sizes(uint64_t nt, uint64_t n[npr::kLevels + 1]) {
   for (int l = 1; l <= npr::kLevels; ++l) n[l] = (n[l - 1] + 63) / 64;
 }
 // group slots after the tile slots: the two-pass kernels' level-1..3 folds, or the resident pass's
-// one aggregate per (virtual) workgroup (rgroups = groups[1], up to ceil(min(nt, 2 kResMaxWaves) /
-// kResWgMin) + 1 slots with the two-segment pass's T0, which can exceed the fold levels'
-// ceil(nt/64) + ceil(nt/4096) + ...)
+// one aggregate per workgroup (rgroups = groups[1], up to ceil(min(nt, kResMaxWaves) / kResWgMin)
+// slots, which can exceed the fold levels' ceil(nt/64) + ceil(nt/4096) + ...)
 static uint64_t group_slots(uint64_t nt) {
   uint64_t n[npr::kLevels + 1];
   level_sizes(nt, n);
   uint64_t folds = 0;
   for (int l = 1; l <= npr::kLevels; ++l) folds += n[l];
-  const uint64_t res = (std::min<uint64_t>(nt, 2 * npr::kResMaxWaves) + npr::kResWgMin - 1) / npr::kResWgMin + 1;
+  const uint64_t res = (std::min<uint64_t>(nt, npr::kResMaxWaves) + npr::kResWgMin - 1) / npr::kResWgMin;
   return std::max(folds, res);
 }
 // tile slots, then the group slots: one allocation (granules are epoch-tagged, so the layout may
@@ -273,8 +269,6 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   }
   const char *env = getenv("NPR_RESIDENT");
   if (env && env[0] == '0') c->resident = 0;
-  env = getenv("NPR_SEGS");
-  if (env && (env[0] == '1' || env[0] == '2')) c->segs = env[0] - '0';
   *out = c;
   return NPR_OK;
 }
@@ -322,10 +316,6 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
     case NPR_OPT_RESIDENT:  // 0 off, 1 auto, N > 1: at most N waves (tests: long ranges, deferral)
       if (value < 0) return fail(c, NPR_ERR_ARG, "NPR_OPT_RESIDENT must be >= 0");
       c->resident = value;
-      return NPR_OK;
-    case NPR_OPT_SEGMENTS:  // 1: the one-segment resident pass only; 2 (default): two segments where they apply
-      if (value != 1 && value != 2) return fail(c, NPR_ERR_ARG, "NPR_OPT_SEGMENTS must be 1 or 2");
-      c->segs = value;
       return NPR_OK;
     case NPR_OPT_PIPE:  // the pipelined pass was an experiment: not in this library
       if (value == 0) return NPR_OK;
@@ -657,20 +647,15 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     p.rslots = (npr::RangeSlot *)c->slots.p;
     p.rgroups = p.groups[1];
     p.pack = c->res_pack ? 1u : 0u;
-    // the two-segment pass: whole 16-wave workgroups, every virtual wave >= 1 tile
-    if (c->segs == 2 && c->seg_ok && !p.pack && wv % npr::kResWgMin == 0 && nt >= 2 * wv) {
-      p.segs = 2;
-      p.nwaves = (uint32_t)(2 * wv);
-    }
-    // every workgroup aggregate the launch writes (+ T0) must lie inside the slot allocation
-    const uint64_t nb = (p.nwaves + npr::kResWgMin - 1) / npr::kResWgMin + (p.segs == 2 ? 1 : 0);
+    // every workgroup aggregate the launch writes must lie inside the slot allocation
+    const uint64_t nb = (wv + npr::kResWgMin - 1) / npr::kResWgMin;
     if ((const char *)(p.rgroups + nb) > (const char *)c->slots.p + c->slots.cap)
       return fail(c, NPR_ERR_ARG, "internal: resident workgroup slots exceed the workspace (%llu groups)",
                   (unsigned long long)nb);
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
   }
   if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_extract(p, s); }))) return st;
-  c->last_pass = !resident ? 1 : p.segs == 2 ? 3 : 2;
+  c->last_pass = resident ? 2 : 1;
   log_summary(c, o->summary);  // who wrote which summary (npr_dev_check, chained launches check it)
   return NPR_OK;
 }

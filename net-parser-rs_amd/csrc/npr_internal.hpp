@@ -127,8 +127,6 @@ struct ParseParams {
   uint32_t pack;           // resident pass: sparse tiles share kept rounds (k_parse_resident<.., true>)
   const npr_summary *prev; // chained launch (resident pass only): continue the chain and the counts
   uint32_t prev_epoch;     //   of the launch that wrote *prev (its epoch, 0 = unchecked); NULL = none
-  uint32_t segs;           // 2: the two-segment resident pass (k_parse_seg; nwaves = 2 x physical waves,
-                           //   a multiple of 32, <= ntiles; rgroups holds 2 nwaves/32 + 1 slots)
 };
 
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)
@@ -142,9 +140,8 @@ struct BatchParams {
   ParseParams p[kMaxBatch];
 };
 hipError_t launch_parse_batch(const BatchParams &bp, hipStream_t s);
-// resident waves per CU the hardware admits for k_parse_resident / k_parse_seg (occupancy query)
+// resident waves per CU the hardware admits for k_parse_resident (occupancy query)
 int resident_waves_per_cu();
-int seg_waves_per_cu();
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                 uint32_t *flows, uint32_t *flows_v6, uint8_t *status,
                                 hipStream_t s);

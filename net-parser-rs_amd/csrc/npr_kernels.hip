@@ -2111,489 +2111,6 @@ __global__ __launch_bounds__(kResWg * kWave) void k_parse_batch(BatchParams bp) 
   }
 }
 
-// =============================================================================================
-// TWO-SEGMENT RESIDENT PASS — k_parse_seg (flows-only launches, the default when every wave gets
-// at least two tiles and no kept round is shared).  The capture's tiles split into two halves
-// (segments).  Physical wave v runs virtual wave v of segment 0, then virtual wave P + v of
-// segment 1 (P = physical waves), each segment's flows in its half of the kept rounds.  So the
-// look-back of segment 0 overlaps the parse of segment 1:
-//   - the LAST wave of a workgroup to finish segment 0 folds the 16 aggregates A(0) in LDS and
-//     publishes G(0, b) while the others already parse segment 1;
-//   - after phase A the lower G(0, .) have long been published, so segment 0's prefixes, and
-//     its rows, follow the workgroup's own phase A by one round trip;
-//   - segment 1's look-back (segment 0's total T0 = all of G(0, .), then the lower G(1, .)) runs
-//     while the other waves write segment 0's rows.
-// In the virtual numbering (waves u = s P + v, workgroups s nb + b; kp.nwaves = 2 P) every slot,
-// fold and re-walk path of the one-segment pass applies unchanged.
-// =============================================================================================
-constexpr int kSegSlots = kResSlots / 2;  // kept rounds per segment
-static_assert(kSegSlots * 8 * 64 * 4 <= (int)sizeof(ResShared), "a segment's kept rounds fit one wave's rings");
-
-struct ResSegShared {
-  ResShared w[kResWg];
-  uint32_t prog[kResWg];  // tiles each wave has parsed (~0: done), for fair priorities
-  Seg a[2][kResWg];       // each wave's segment aggregates A(s)
-  Seg x[2][kResWg];       // in-workgroup exclusive prefixes (the last arriver), then the prefixes X(s)
-  Seg g0;                 // this workgroup's segment-0 aggregate G(0, b)
-  uint32_t arr[2];        // waves done with segment s
-  uint32_t ready;         // wave 0's prefixes in LDS: X(0) (>= 1), X(1) (>= 2)
-  uint32_t fail;          // a bounded wait timed out: every wave leaves
-};
-
-// Fold the workgroup aggregates G(gb .. gb + cnt - 1) (cnt <= 64 kTopWin) onto E: every window read
-// at once (sc1 loads), then only the lanes not yet this launch's re-read (returning atomics).
-// spec_anchor: E is anchored at G(gb)'s speculated entry (kFlagSpecStart), reported in entry0.
-__device__ bool seg_lookback(const ParseParams &kp, uint32_t gb, uint32_t cnt, bool spec_anchor, Seg &E,
-                             uint64_t &entry0, uint64_t t0) {
-  const uint32_t lane = threadIdx.x & 63u;
-  LaneSeg G[kTopWin];
-#pragma unroll
-  for (int w = 0; w < kTopWin; ++w) {  // descending inside a window (fold_window's order)
-    const uint32_t w0 = 64u * (uint32_t)w, sz = cnt > w0 ? (cnt - w0 < 64u ? cnt - w0 : 64u) : 0u;
-    G[w] = load_res(kp, 1, (int64_t)gb + w0 + sz - 1 - lane, lane < sz, true);
-  }
-  bool okw = true;
-  uint32_t nap = 1;
-  for (int tries = 0;; ++tries) {
-    bool miss = false;
-#pragma unroll
-    for (int w = 0; w < kTopWin; ++w) {
-      const uint32_t w0 = 64u * (uint32_t)w, sz = cnt > w0 ? (cnt - w0 < 64u ? cnt - w0 : 64u) : 0u;
-      miss = miss || __ballot(lane < sz && !G[w].present) != 0ull;
-    }
-    if (!miss) break;
-    if (tries && !res_nap(kp, t0, nap)) {
-      okw = false;
-      break;
-    }
-#pragma unroll
-    for (int w = 0; w < kTopWin; ++w) {
-      const uint32_t w0 = 64u * (uint32_t)w, sz = cnt > w0 ? (cnt - w0 < 64u ? cnt - w0 : 64u) : 0u;
-      const bool need = lane < sz && !G[w].present;
-      if (__ballot(need)) {
-        const LaneSeg N = load_res(kp, 1, (int64_t)gb + w0 + sz - 1 - lane, need);
-        if (need) G[w] = N;
-      }
-    }
-  }
-  if (spec_anchor && cnt) {
-    entry0 = rl64(G[0].entry, (int)(cnt < 64u ? cnt : 64u) - 1);
-    E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
-  }
-#pragma unroll
-  for (int w = 0; w < kTopWin; ++w) {
-    const uint32_t w0 = 64u * (uint32_t)w;
-    if (w0 >= cnt || !okw) break;
-    E = combine(kp, E, fold_window(kp, G[w], (int)(cnt - w0 < 64u ? cnt - w0 : 64u) - 1));
-  }
-  return okw;
-}
-
-// DIAG: per physical wave (stamps row u0) s_memrealtime at [0] start, [1] first tile landed, [2]
-// segment 0 parsed, [3] its A published (and folded, by the last arriver: [12] = 1), [4] phase A
-// done, [5] past the barrier, [6] wave 0: segment 0's prefixes and T0 known, [7] phase B of segment
-// 0 starts, [8] wave 0: segment 1's prefixes known, [9] segment 0's rows written, [10] phase B of
-// segment 1 starts, [11] done; [13] phase A ticks waiting for tiles, [14] n0, [15] tiles.
-template <bool DIAG>
-__device__ __forceinline__ bool res_capture_seg(const ParseParams &kp, ResSegShared &sh) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar LDS bases
-  const uint32_t b = blockIdx.x, nbp = gridDim.x;  // physical workgroups (virtual: s nbp + b)
-  const uint32_t P = nbp * kResWg;                 // physical waves (kp.nwaves = 2 P)
-  const uint32_t u0 = b * kResWg + wid, u1 = P + u0;
-  if (wid == 0 && lane == 0) {
-    sh.arr[0] = 0u;
-    sh.arr[1] = 0u;
-    sh.ready = 0u;
-    sh.fail = 0u;
-  }
-  __syncthreads();  // (no DMA in flight yet: a plain barrier)
-  Stamps st;
-  if (DIAG) {
-    for (int i = 0; i < kStampWords; ++i) st.v[i] = 0;
-    stamp_at(st, 0);
-  }
-  uint64_t wait_ticks = 0;
-  uint32_t a0, a1, d0, d1;
-  res_range(kp, u0, a0, a1);
-  res_range(kp, u1, d0, d1);
-  const uint32_t n0 = a1 - a0, ntot = n0 + (d1 - d0);  // n0 >= 1: the host asks for ntiles >= kp.nwaves
-  const uint64_t base0 = kp.org + (uint64_t)a0 * kTile, base1 = kp.org + (uint64_t)d0 * kTile;
-  auto tile_of = [&](uint32_t k) -> uint64_t {
-    return k < n0 ? base0 + (uint64_t)k * kTile : base1 + (uint64_t)(k - n0) * kTile;
-  };
-  const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;
-  if (lane == 0) sh.prog[wid] = 0u;
-  const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
-#pragma unroll
-  for (int k = 0; k < kResRing - 1; ++k)
-    if ((uint32_t)k < ntot) dma_tile<2>(kp, tile_of((uint32_t)k), sh.w[wid].data[k]);
-  __builtin_amdgcn_s_setprio(3);
-
-  // ---- phase A: segment 0's range, then segment 1's, through one DMA ring ---------------------
-  uint32_t fl[kResSlots][8];              // kept rounds (segment s: rounds s kSegSlots ..), as k_parse_resident
-  uint32_t m_ok = 0, m_lo = 0, m_hi = 0;  // lane q: Ok flows of its segment before kept round q, its Ok ballot
-  uint32_t sb = 0, ns = 0;                // the segment's first kept round; kept rounds used
-  uint64_t entry = kNone, pos = kNone;
-  bool ended = false;
-  uint32_t cnt = 0, okc = 0;
-  uint32_t c1 = a1;
-  uint32_t tdef = c1, cdef = 0, odef = 0;
-  uint64_t pdef = 0;
-  uint32_t wlast = kAnyLen;
-  // segment 0 once parsed
-  uint64_t entry_0 = kNone, pos_0 = kNone, pdef_0 = 0;
-  uint32_t cnt_0 = 0, okc_0 = 0, ns_0 = 0, tdef_0 = a1, cdef_0 = 0, odef_0 = 0;
-  SpecCtx sc{};
-
-  // A(s) into LDS; the workgroup's last wave to get here folds the 16 and publishes G(s, b)
-  auto seg_done = [&](uint32_t s, uint32_t r0, uint32_t r1) {
-    if (lane == 0) {
-      Seg A;
-      A.entry = entry;
-      A.exit = pos == kNone ? 0ull : pos;
-      A.cnt = cnt;
-      A.ok = okc;
-      A.first = r0;
-      A.last = (int64_t)r1 - 1;
-      A.mism = -1;
-      A.valid = true;
-      A.spare = 0;
-      sh.a[s][wid] = A;
-    }
-    uint32_t old = 0;
-    if (lane == 0) old = __hip_atomic_fetch_add(&sh.arr[s], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-    old = (uint32_t)__builtin_amdgcn_readfirstlane(old);
-    if (DIAG && s == 0) st.v[12] = old == kResWg - 1u;
-    if (old == kResWg - 1u) {
-      LaneSeg L{};
-      L.mism = -1;
-      L.valid = true;
-      if (lane < kResWg) {
-        const Seg &A = sh.a[s][lane];
-        L.entry = A.entry;
-        L.exit = A.exit;
-        L.cnt = A.cnt;
-        L.ok = A.ok;
-        L.first = A.first;
-        L.last = A.last;
-        L.present = true;
-      }
-      Seg e, agg;
-      res_fold_lanes(kp, L, (int)kResWg, e, agg);
-      if (lane == 0) put_agg(kp, kp.rgroups + s * nbp + b, agg);
-      if (lane < kResWg) sh.x[s][lane] = e;
-      if (s == 0 && lane == 0) sh.g0 = agg;
-    }
-  };
-
-  for (uint32_t k = 0; k < ntot; ++k) {
-    if (k == n0) {  // segment 0 parsed: keep its state, publish A(0), go on with segment 1
-      if (DIAG) stamp_at(st, 2);
-      entry_0 = entry;
-      pos_0 = pos;
-      cnt_0 = cnt;
-      okc_0 = okc;
-      ns_0 = ns;
-      tdef_0 = tdef;
-      pdef_0 = pdef;
-      cdef_0 = cdef;
-      odef_0 = odef;
-      seg_done(0, a0, a1);
-      if (DIAG) stamp_at(st, 3);
-      sb = kSegSlots;
-      ns = 0;
-      entry = pos = kNone;
-      ended = false;
-      cnt = okc = 0;
-      c1 = d1;
-      tdef = c1;
-      pdef = 0;
-      cdef = odef = 0;
-      wlast = kAnyLen;
-    }
-    const uint32_t slot = k % kResRing;
-    const uint32_t t = k < n0 ? a0 + k : d0 + (k - n0);
-    const uint64_t seg_base = k < n0 ? base0 : base1;
-    const uint64_t tile_lo = kp.org + (uint64_t)t * kTile;
-    const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    if (k + kResRing - 1 < ntot)
-      dma_tile<2>(kp, tile_of(k + kResRing - 1), sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
-    const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    res_wait<0>(ntot - 1 - k < (uint32_t)(kResRing - 1) ? ntot - 1 - k : (uint32_t)(kResRing - 1));
-    if (DIAG) wait_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
-    if (k == 0) {
-      sc = spec_ctx(kp, scb);
-      if (DIAG) stamp_at(st, 1);
-    }
-    const uint32_t *w = sh.w[wid].data[slot];
-    if (!ended) {
-      if (pos == kNone) {
-        uint64_t e;
-        if (t == 0 && !spec0) {
-          e = kp.start;
-        } else {
-          const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;
-          e = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
-        }
-        e = uni64(e);
-        if (e != kNone) entry = pos = e;
-      }
-      if (pos != kNone && pos < tile_hi) {
-        uint32_t n = 0;
-        const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n, &wlast));
-        wave_sync();
-        const uint32_t rounds = (n + 63u) >> 6;
-        if (tdef == c1 && ns + rounds > (uint32_t)kSegSlots) {  // out of this segment's rounds: defer the rest
-          tdef = t;
-          pdef = pos;
-          cdef = cnt;
-          odef = okc;
-        }
-        if (tdef == c1) {
-          for (uint32_t s = 0; s < rounds; ++s) {
-            const uint32_t qu = __builtin_amdgcn_readfirstlane(sb + ns);  // uniform: one scalar branch per slot
-            const uint32_t i = lane + s * 64u;
-            const bool valid = i < n;
-            FlowWords f;
-            const uint32_t rel = sh.w[wid].srec[i];
-            const bool okr = decode_rec<true>(kp, w, tile_lo, rel, f, valid) == NPR_FLOW_OK && valid;
-            const uint64_t bal = __ballot(okr);
-            const uint32_t sw[8] = {(f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3],
-                                    f.d[4], f.d[5], f.d[6], (uint32_t)(tile_lo + rel - seg_base)};
-#pragma unroll
-            for (int q = 0; q < kResSlots; ++q)
-              if ((uint32_t)q == qu) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) fl[q][j] = sw[j];
-              }
-            m_ok = lane == qu ? okc : m_ok;
-            m_lo = lane == qu ? (uint32_t)bal : m_lo;
-            m_hi = lane == qu ? (uint32_t)(bal >> 32) : m_hi;
-            ++ns;
-            okc += (uint32_t)__builtin_popcountll(bal);
-          }
-        } else {  // deferred: status only (the Ok count), flows re-read in phase B
-          for (uint32_t s = 0; s < rounds; ++s) {
-            const uint32_t i = lane + s * 64u;
-            const bool valid = i < n;
-            FlowWords f;
-            const bool okr = decode_rec<false>(kp, w, tile_lo, sh.w[wid].srec[i], f, valid) == NPR_FLOW_OK && valid;
-            okc += (uint32_t)__builtin_popcountll(__ballot(okr));
-          }
-        }
-        cnt += n;
-        ended = ex < tile_hi;  // Err(Incomplete): the chain stops here (Q3)
-        pos = ex;
-      }
-    }
-    wave_sync();  // done with this slot before it is refilled
-    // fair priorities, as k_parse_resident (short ranges step down after each of the first tiles)
-    if (ntot <= kStepPrioTiles) {
-      if (k == 0) __builtin_amdgcn_s_setprio(2);
-      else if (k == 1) __builtin_amdgcn_s_setprio(1);
-      else if (k == 2) __builtin_amdgcn_s_setprio(0);
-    } else if ((k & 3u) == 3u) {
-      if (lane == 0) sh.prog[wid] = k + 1;
-      uint32_t mn = lane < kResWg ? sh.prog[lane] : ~0u;
-#pragma unroll
-      for (int o = 1; o < (int)kResWg; o <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
-      const uint32_t dd = k + 1 - __builtin_amdgcn_readfirstlane(mn);
-      if (dd == 0) __builtin_amdgcn_s_setprio(3);
-      else if (dd == 1) __builtin_amdgcn_s_setprio(2);
-      else if (dd == 2) __builtin_amdgcn_s_setprio(1);
-      else __builtin_amdgcn_s_setprio(0);
-    }
-  }
-  if (lane == 0) sh.prog[wid] = ~0u;
-  const uint32_t ep = kp.epoch;
-  if (lane == 0) {  // A words in HBM (the rare generic prefix reads them)
-    RangeSlot *r0 = kp.rslots + u0, *r1 = kp.rslots + u1;
-    st_agent(&r0->a[0], gran(ep, pos_0 == kNone ? 0ull : pos_0));
-    st_agent(&r0->a[1], gran(ep, entry_0 == kNone ? 0ull : entry_0 + 1));
-    st_agent(&r0->a[2], gran(ep, cnt_0));
-    st_agent(&r0->a[3], gran(ep, okc_0));
-    st_agent(&r1->a[0], gran(ep, pos == kNone ? 0ull : pos));
-    st_agent(&r1->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
-    st_agent(&r1->a[2], gran(ep, cnt));
-    st_agent(&r1->a[3], gran(ep, okc));
-  }
-  if (DIAG) stamp_at(st, 4);
-  seg_done(1, d0, d1);
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  __syncthreads();  // every G(s, b) of this workgroup is published, every X-in-workgroup in LDS
-  if (DIAG) stamp_at(st, 5);
-
-  if (wid == 0) {
-    // Wave 0 resolves both segments' prefixes.  Its kept rounds wait in the idle rings (segment 0's
-    // in wave 1's, segment 1's in its own) so that the windows get the registers.
-    uint32_t *st0 = &sh.w[1].data[0][0], *st1 = &sh.w[0].data[0][0];
-#pragma unroll
-    for (int q = 0; q < kSegSlots; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        st0[(q * 8 + j) * 64 + lane] = fl[q][j];
-        st1[(q * 8 + j) * 64 + lane] = fl[kSegSlots + q][j];
-      }
-    // (1) segment 0: E(0, b) = anchor ⊕ G(0, 0 .. b-1)
-    Seg E = start_seg(kp);
-    uint64_t entry0 = kp.start;
-    bool okw = true;
-    const bool spec_anchor = (kp.flags & kFlagSpecStart) && !kp.prev;
-    if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
-      okw = kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch;
-      entry0 = kp.prev->entry;
-      E.entry = E.exit = kp.prev->consumed;
-      E.cnt = kp.prev->n_records;
-      E.ok = kp.prev->n_flows;
-    } else if (spec_anchor && b == 0) {
-      entry0 = sh.a[0][0].entry;
-      E.entry = E.exit = entry0 == kNone ? kp.stop : entry0;
-    }
-    okw = okw && seg_lookback(kp, 0, b, spec_anchor, E, entry0, t0);
-    if (lane < kResWg) sh.x[0][lane] = lane == 0 ? E : combine(kp, E, sh.x[0][lane]);
-    if (b == nbp - 1 && lane == 0) kp.summary->entry = entry0;
-    // T0 = segment 0 whole: E(0, b) ⊕ G(0, b) ⊕ the higher workgroups' G(0, .), all published at
-    // their segment-0 ends (folded here: no hop through another workgroup)
-    Seg T = combine(kp, E, sh.g0);
-    if (okw && b + 1 < nbp) {
-      uint64_t unused = 0;
-      okw = seg_lookback(kp, b + 1, nbp - 1 - b, false, T, unused, t0);
-    }
-    if (DIAG) stamp_at(st, 6);
-#pragma unroll
-    for (int q = 0; q < kSegSlots; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fl[q][j] = st0[(q * 8 + j) * 64 + lane];
-    if (lane == 0) {
-      sh.fail = okw ? 0u : 1u;
-      __hip_atomic_store(&sh.ready, okw ? 1u : 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    // (2) segment 1: E(1, b) = T0 ⊕ G(1, 0 .. b-1), while the other waves write segment 0's rows
-    if (okw) {
-      uint64_t unused = 0;
-      okw = seg_lookback(kp, nbp, b, false, T, unused, t0);
-      if (lane < kResWg) sh.x[1][lane] = lane == 0 ? T : combine(kp, T, sh.x[1][lane]);
-      if (lane == 0) {
-        sh.fail = okw ? 0u : 1u;
-        __hip_atomic_store(&sh.ready, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    if (DIAG) stamp_at(st, 8);
-#pragma unroll
-    for (int q = 0; q < kSegSlots; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) fl[kSegSlots + q][j] = st1[(q * 8 + j) * 64 + lane];
-  }
-
-  // ---- phase B: segment 0's rows, then segment 1's -----------------------------------------------
-  auto wait_ready = [&](uint32_t lvl) -> bool {
-    while (__hip_atomic_load(&sh.ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < lvl)
-      __builtin_amdgcn_s_sleep(2);
-    return __hip_atomic_load(&sh.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u;
-  };
-  auto phase_b = [&](uint32_t s, uint32_t u, uint32_t c0s, uint32_t c1s, uint64_t base, uint64_t entry_s,
-                     uint64_t pos_s, uint32_t cnt_s, uint32_t okc_s, uint32_t ns_s, uint32_t tdef_s, uint64_t pdef_s,
-                     uint32_t cdef_s, uint32_t odef_s) -> bool {
-    Seg X = sh.x[s][wid];
-    if (!X.valid && !res_prefix(kp, u, X, t0)) return false;
-    const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1s - 1);
-    uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
-    const bool before_end = X.exit < tile_end(kp, X.last);  // the chain ended before this range
-    if (!before_end && xe < range_hi && xe >= range_lo) {
-      if (entry_s != kNone && xe == entry_s) {  // the speculated chain is the exact one: flows from registers
-        if (kp.flows) {
-          const uint32_t q0 = s * (uint32_t)kSegSlots;
-#pragma unroll
-          for (int q = 0; q < kResSlots; ++q) {
-            if ((uint32_t)q >= q0 && (uint32_t)q < q0 + ns_s) {
-              const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
-              const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
-                                   (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
-              // the round's Ok rows are one contiguous block: staged in the idle ring slot in address
-              // order, stored as whole lines, non-temporally (k_parse_resident's phase B)
-              const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
-              const uint64_t f0 = xo + okb;
-              if (nok && f0 + nok <= kp.flow_cap) {
-                const bool mine = (bal >> lane) & 1ull;
-                const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-                const uint64_t p = base + fl[q][7];
-                const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-                u32x4 *stg = reinterpret_cast<u32x4 *>(sh.w[wid].data[0]);
-                if (mine) {
-                  const uint32_t kk = nok - 1u - rank;  // rank r lands at row flow_cap - 1 - (f0 + r)
-                  stg[stg_slot<128>(2 * kk)] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
-                  stg[stg_slot<128>(2 * kk + 1)] =
-                      u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
-                }
-                wave_sync();
-                u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
-                if (lane < 2u * nok) __builtin_nontemporal_store(stg[stg_slot<128>(lane)], dst + lane);
-                if (lane + 64u < 2u * nok)
-                  __builtin_nontemporal_store(stg[stg_slot<128>(lane + 64)], dst + lane + 64);
-                if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
-                wave_sync();  // the slot is rewritten by the next round
-              } else if ((bal >> lane) & 1ull) {
-                const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-                if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
-              }
-            }
-          }
-        }
-        if (tdef_s < c1s) {
-          uint64_t dc = xc + cdef_s, dok = xo + odef_s;
-          (void)res_emit(kp, sh.w[wid], tdef_s, c1s, pdef_s, dc, dok);
-          if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1s - tdef_s);
-        }
-        xe = pos_s;
-        xc += cnt_s;
-        xo += okc_s;
-      } else {  // mis-speculated: re-read the whole range from the exact position
-        xe = uni64(res_emit(kp, sh.w[wid], c0s, c1s, xe, xc, xo));
-        if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1s - c0s);
-      }
-    }
-    if (lane == 0) {
-      RangeSlot *rs = kp.rslots + u;
-      st_agent(&rs->p[0], gran(ep, xe));
-      st_agent(&rs->p[1], gran(ep, xc));
-      st_agent(&rs->p[2], gran(ep, xo));
-      if (u == kp.nwaves - 1) {
-        uint32_t fl2 = 0;
-        if (kp.flows && xo > kp.flow_cap) fl2 |= NPR_SUMMARY_FLOW_OVERFLOW;
-        kp.summary->n_records = xc;
-        kp.summary->n_flows = xo;
-        kp.summary->consumed = xe;
-        kp.summary->flags = fl2;
-        kp.summary->epoch = ep;
-      }
-    }
-    return true;
-  };
-  if (!wait_ready(1u)) return false;
-  if (DIAG) stamp_at(st, 7);
-  if (!phase_b(0, u0, a0, a1, base0, entry_0, pos_0, cnt_0, okc_0, ns_0, tdef_0, pdef_0, cdef_0, odef_0)) return false;
-  if (DIAG) stamp_at(st, 9);
-  if (!wait_ready(2u)) return false;
-  if (DIAG) stamp_at(st, 10);
-  const bool ok = phase_b(1, u1, d0, d1, base1, entry, pos, cnt, okc, ns, tdef, pdef, cdef, odef);
-  if (DIAG) {
-    stamp_at(st, 11);
-    st.v[13] = wait_ticks;
-    st.v[14] = n0;
-    st.v[15] = ntot;
-    stamp_flush(kp, st, u0, 0xFFFFu);
-  }
-  return ok;
-}
-
-template <bool DIAG>
-__global__ __launch_bounds__(kResWg * kWave) void k_parse_seg(ParseParams kp) {
-  __shared__ __attribute__((aligned(16))) ResSegShared sh;
-  (void)res_capture_seg<DIAG>(kp, sh);
-}
-
-
 int resident_waves_per_cu() {
   int nb = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_resident<false, false>), kResWg * kWave, 0) !=
@@ -2611,21 +2128,7 @@ static hipError_t launch(const ParseParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
-int seg_waves_per_cu() {
-  int nb = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void *>(&k_parse_seg<false>), kResWg * kWave, 0) !=
-      hipSuccess)
-    return 0;
-  return nb * (int)kResWg;
-}
-
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
-  if (p.nwaves && p.segs == 2) {  // virtual waves: two per physical wave
-    if (p.nwaves % (2 * kResWg) || p.ntiles < p.nwaves || p.pack) return hipErrorInvalidValue;
-    auto k = (p.stats || p.stamps) ? k_parse_seg<true> : k_parse_seg<false>;
-    hipLaunchKernelGGL(k, dim3(p.nwaves / (2 * kResWg)), dim3(kResWg * kWave), 0, s, p);
-    return hipGetLastError();
-  }
   if (p.nwaves) {
     const uint32_t nb = (p.nwaves + kResWg - 1) / kResWg;
     const bool diag = p.stats || p.stamps;

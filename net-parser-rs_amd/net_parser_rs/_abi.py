@@ -44,8 +44,7 @@ VXLAN_PORT_IANA = 4789
 OPT_PIPE = 4  # npr_ctx_set_option: the pipelined pass (an experiment) is not built: only 0 is accepted
 OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's device window in chunks (0 auto, >= 3)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
-OPT_SEGMENTS = 6  # npr_ctx_set_option: 2 (default) the two-segment resident pass where it applies, 1 never
-PASS_TWO_PASS, PASS_RESIDENT, PASS_SEGMENTED, PASS_BATCH = 1, 2, 3, 4  # npr_ctx_last_pass
+PASS_TWO_PASS, PASS_RESIDENT, PASS_BATCH = 1, 2, 4  # npr_ctx_last_pass
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1
 

@@ -104,18 +104,12 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
         ctx = npr.context(0)
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SEGMENTS, 2))
         try:
             sm = check_parity(blob, start, endianness, ws, light=True)
         finally:
             ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SEGMENTS, 1))
-        # the pass that ran: two segments when the waves are whole workgroups and each gets >= 2 tiles
-        org = start - start % 4096
-        nt = max(1, -(-(len(blob) - org) // 4096))
-        want = (_abi.PASS_TWO_PASS if light == "decode" else
-                _abi.PASS_SEGMENTED if light % 16 == 0 and nt >= 2 * light else _abi.PASS_RESIDENT)
-        assert ctx.lib.npr_ctx_last_pass(ctx.handle) == want, (ctx.lib.npr_ctx_last_pass(ctx.handle), want, nt)
+        want = _abi.PASS_TWO_PASS if light == "decode" else _abi.PASS_RESIDENT  # the pass that ran
+        assert ctx.lib.npr_ctx_last_pass(ctx.handle) == want, (ctx.lib.npr_ctx_last_pass(ctx.handle), want)
         return sm
     want = expect(blob, start, endianness)
     want_recs, want_cons, want_flows, want_v6, want_status, e = want
@@ -173,13 +167,10 @@ def test_kat_frames_as_records(name):
 
 
 # ---- synthetic corpora ---------------------------------------------------------------------
-# resident_w16 / _w48 / _w256: the two-segment pass (whole 16-wave workgroups) with 1, 3 and 16
-# workgroups: long ranges with deferred tiles (3 kept rounds per segment), segment 1's look-back over
-# segment 0's total from the last workgroup
-LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, 256, "decode", "batch", "batch_w7",
-                                          "batch_w100"],
-                                ids=["full", "resident", "resident_w7", "resident_w100", "seg_w16", "seg_w48",
-                                     "seg_w256", "two_pass", "batch", "batch_w7", "batch_w100"])
+# resident_w16 / _w48: whole 16-wave workgroups (one and three), long ranges with deferred tiles
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode", "batch", "batch_w7", "batch_w100"],
+                                ids=["full", "resident", "resident_w7", "resident_w100", "resident_w16",
+                                     "resident_w48", "two_pass", "batch", "batch_w7", "batch_w100"])
 
 
 @LIGHT

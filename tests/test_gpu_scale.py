@@ -49,23 +49,16 @@ def v6_rows(flows, v6):
     return v6[m]
 
 
-@pytest.mark.parametrize("segs", [2, 1], ids=["two_segments", "one_segment"])
-def test_c2_bench_launch_bit_exact(segs):
-    """The exact launch bench.py times: 1M records, one resident dispatch (k_parse_seg, the
-    default; k_parse_resident with NPR_OPT_SEGMENTS = 1)."""
+def test_c2_bench_launch_bit_exact():
+    """The exact launch bench.py times: 1M records, one k_parse_resident dispatch."""
     blob = synth.fixed64(1_000_000)
     hdr, recs, cons, flows, _ = oracle_flows(blob)
     n = len(recs)
     ws = device.Workspace(record_cap=n, flow_cap=n, records=False, offsets=False, status=False,
                           flows=True, flows_v6=True)
-    ctx = ws.ctx
-    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SEGMENTS, segs))
-    try:
-        ws.launch(to_dev(blob), start=24, endianness=hdr.endianness)
-        sm = ws.check()
-        assert ctx.lib.npr_ctx_last_pass(ctx.handle) == (_abi.PASS_SEGMENTED if segs == 2 else _abi.PASS_RESIDENT)
-    finally:
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SEGMENTS, 1))
+    ws.launch(to_dev(blob), start=24, endianness=hdr.endianness)
+    sm = ws.check()
+    assert ws.ctx.lib.npr_ctx_last_pass(ws.ctx.handle) == _abi.PASS_RESIDENT
     assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons)
     assert ws.flows_np().tobytes() == flows.tobytes()
 
