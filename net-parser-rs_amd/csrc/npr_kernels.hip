@@ -2629,9 +2629,11 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
   }
 }
 
-// 4 records per lane, one staged window at a time: measured best on C2 (37.6 us per 1M records;
+// 4 records per lane, one staged window at a time (the next one prefetched into registers): measured
+// best on C2 (37.6 us per 1M records before the row staging and the prefetch, 28.5 us with them;
 // 1 / 2 records per lane 53.7 / 41.9 us, 4 with two windows staged at once 47.7 us: LDS-bound
-// occupancy)
+// occupancy; a persistent kernel writing each round's rows while the next round loads, 29.9 us:
+// profiles/r03_convert_experiment_ab.json)
 constexpr int kCvtPer = 4, kCvtRows = 1;
 uint64_t convert_blocks(uint64_t n) {
   const uint64_t r = (uint64_t)kBlock * kCvtPer;
