@@ -82,6 +82,23 @@ def main():
         call()
     host_ms = (time.perf_counter() - t0) * 1e3 / reps
     assert k.value == len(want_f) and hf.tobytes() == want_f.tobytes()
+    # FlowExtraction::extract_flow one record at a time (what the Rust crate's per-record trait
+    # method does): one npr_extract_flows host call per record, its 80-B record as the input
+    one = np.frombuffer(blob, np.uint8)[24:24 + 80].copy()
+    r1 = np.zeros(1, _abi.RECORD_DTYPE)
+    r1[0] = (0, 0, 0, 64, 64)
+    f1 = np.zeros(1, _abi.FLOW_DTYPE)
+    v1 = np.zeros(1, _abi.FLOW_V6_DTYPE)
+    s1 = np.zeros(1, np.uint8)
+    call1 = lambda: ctx.check(ctx.lib.npr_extract_flows(ctx.handle, one.ctypes.data, one.size, r1.ctypes.data, 1,
+                                                        f1.ctypes.data, v1.ctypes.data, s1.ctypes.data))
+    call1()
+    reps1 = 200
+    t0 = time.perf_counter()
+    for _ in range(reps1):
+        call1()
+    per_call_us = (time.perf_counter() - t0) * 1e6 / reps1
+    assert s1[0] == 0 and f1[0].tobytes()[:27] == want_f[-1].tobytes()[:27]  # record 0 (the last row), offset aside
     # the CPU oracle on the same list
     t0 = time.perf_counter()
     passes = 0
@@ -115,6 +132,10 @@ def main():
         "dev_flow_aggregate": {"c2_all_distinct_ms": round(agg_ms, 5), "zipf_5000_flows_ms": round(agg_mix_ms, 5),
                                "rows": n, "zipf_rows": nm,
                                "Mrows_per_s": round(n / agg_ms / 1e3, 1)},
+        "host_extract_flow_one_record": {"us_per_call": round(per_call_us, 1),
+                                         "note": "one npr_extract_flows host call per record (the Rust "
+                                                 "FlowExtraction::extract_flow default method): H2D + launch + D2H + "
+                                                 "sync; use extract_flows / convert_records for batches"},
         "host_convert_records": {"ms": round(host_ms, 3), "Mrecords_per_s": round(n / host_ms / 1e3, 1),
                                  "note": "pageable host buffers: capture + records H2D, flow rows D2H"},
         "cpu_oracle_convert_records": {"ms": round(cpu_ms, 3), "Mrecords_per_s": round(n / cpu_ms / 1e3, 2),
