@@ -6,7 +6,7 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CRATE = "rust/net-parser-rs-amd"
 FILES = [("Cargo.toml", "toml"), ("build.rs", "rust"), ("src/ffi.rs", "rust"), ("src/lib.rs", "rust"),
-         ("src/flow.rs", "rust")]
+         ("src/types.rs", "rust"), ("src/flow.rs", "rust")]
 MARK = "## 2. The crate, file by file"
 TAIL = "## 3. "
 

@@ -13,7 +13,7 @@ CRATE = os.path.join(REPO, "rust", "net-parser-rs-amd")
 def test_integration_md_quotes_the_committed_crate():
     doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
     blocks = re.findall(r"### `rust/net-parser-rs-amd/([^`]+)`\n\n````[a-z]+\n(.*?)````\n", doc, re.S)
-    assert {f for f, _ in blocks} == {"Cargo.toml", "build.rs", "src/ffi.rs", "src/lib.rs", "src/flow.rs"}
+    assert {f for f, _ in blocks} == {"Cargo.toml", "build.rs", "src/ffi.rs", "src/lib.rs", "src/types.rs", "src/flow.rs"}
     for f, body in blocks:
         assert body == open(os.path.join(CRATE, f)).read(), f"INTEGRATION.md is stale for {f}: run scripts/gen_integration.py"
 
