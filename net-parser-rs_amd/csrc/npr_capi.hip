@@ -57,6 +57,8 @@ struct npr_ctx {
   std::vector<hipEvent_t> linked;
   npr_summary *sum_host = nullptr;
   uint8_t *head_h = nullptr;  // pinned: the first bytes of a large capture (link sizing)
+  uint8_t *small_h = nullptr;  // pinned arena of the small-call path (small_call)
+  uint64_t small_cap = 0;
   uint64_t sum_host_cap = 0;
   // ... through a bounded device window (NPR_OPT_DEVICE_WINDOW): chunk ring + flow-row ring
   int window = 0;                        // chunks (0 = auto: only when the staged capture would not fit)
@@ -299,6 +301,7 @@ void npr_ctx_destroy(npr_ctx *c) {
   for (hipEvent_t ev : c->row_copied) (void)hipEventDestroy(ev);
   if (c->sum_host) (void)hipHostFree(c->sum_host);
   if (c->head_h) (void)hipHostFree(c->head_h);
+  if (c->small_h) (void)hipHostFree(c->small_h);
   if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
   if (c->d2h_stream) (void)hipStreamDestroy(c->d2h_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -811,6 +814,34 @@ npr_status npr_dev_extract_flows(npr_ctx *c, const void *input, uint64_t len, co
 }
 
 // ---- host-memory entry points ---------------------------------------------------------------
+// Small host calls (a handful of records: the Rust crate's per-record FlowExtraction::extract_flow
+// and its error-payload query) skip the device staging buffers: input and records are packed into
+// one page-locked arena that the kernel reads over PCIe, and it writes its outputs there too, so a
+// call is one launch and one synchronisation instead of five pageable copies (65 us -> see
+// scripts/bench_records_api.py host_extract_flow_one_record).  Arena layout: input | records |
+// then the outputs at the offsets the caller asks for (16-B aligned).
+constexpr uint64_t kSmallBytes = 256u << 10;  // input + records at most this many bytes
+static uint64_t a16(uint64_t x) { return (x + 15) & ~15ull; }
+static npr_status small_arena(npr_ctx *c, const uint8_t *in, size_t len, const npr_record *records, size_t n,
+                              uint64_t out_bytes, uint8_t *&arena, uint64_t &rec_off, uint64_t &out_off) {
+  rec_off = a16(len);
+  out_off = a16(rec_off + n * sizeof(npr_record));
+  const uint64_t need = out_off + out_bytes;
+  if (need > c->small_cap) {
+    if (c->small_h) HIP_CHECK(c, hipHostFree(c->small_h));
+    c->small_h = nullptr;
+    c->small_cap = 0;
+    const uint64_t cap = std::max<uint64_t>(need, 64u << 10);
+    HIP_CHECK(c, hipHostMalloc((void **)&c->small_h, cap, 0));
+    c->small_cap = cap;
+  }
+  arena = c->small_h;
+  if (len) memcpy(arena, in, len);
+  if (n) memcpy(arena + rec_off, records, n * sizeof(npr_record));
+  return NPR_OK;
+}
+static bool small_call(size_t len, size_t n) { return len + n * sizeof(npr_record) <= kSmallBytes; }
+
 static npr_status stage_input(npr_ctx *c, const uint8_t *in, size_t len) {
   npr_status st = ensure(c, c->in, len + 16);
   if (st) return st;
@@ -1280,7 +1311,21 @@ npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const np
                              npr_flow *flows, npr_flow_v6 *flows_v6, uint8_t *status) {
   if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
   HIP_CHECK(c, hipSetDevice(c->device));
-  npr_status st = stage_input(c, in, len);
+  npr_status st;
+  if (n && small_call(len, n)) {  // one launch over the page-locked arena
+    uint8_t *ar = nullptr;
+    uint64_t ro = 0, oo = 0;
+    const uint64_t fo = 0, vo = a16(n * sizeof(npr_flow)), so = vo + a16(n * sizeof(npr_flow_v6));
+    if ((st = small_arena(c, in, len, records, n, so + n, ar, ro, oo))) return st;
+    HIP_CHECK(c, npr::launch_extract_dense(ar, len, (const npr_record *)(ar + ro), n, (uint32_t *)(ar + oo + fo),
+                                           (uint32_t *)(ar + oo + vo), ar + oo + so, c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (flows) memcpy(flows, ar + oo + fo, n * sizeof(npr_flow));
+    if (flows_v6) memcpy(flows_v6, ar + oo + vo, n * sizeof(npr_flow_v6));
+    if (status) memcpy(status, ar + oo + so, n);
+    return NPR_OK;
+  }
+  st = stage_input(c, in, len);
   if (st) return st;
   if (n == 0) return NPR_OK;
   if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
@@ -1303,7 +1348,20 @@ npr_status npr_flow_details(npr_ctx *c, const uint8_t *in, size_t len, const npr
                             uint8_t *status, uint64_t *detail) {
   if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
   HIP_CHECK(c, hipSetDevice(c->device));
-  npr_status st = stage_input(c, in, len);
+  npr_status st;
+  if (n && small_call(len, n)) {  // one launch over the page-locked arena
+    uint8_t *ar = nullptr;
+    uint64_t ro = 0, oo = 0;
+    const uint64_t so = a16(n * sizeof(uint64_t));  // details first (8-B aligned), then status
+    if ((st = small_arena(c, in, len, records, n, so + n, ar, ro, oo))) return st;
+    HIP_CHECK(c, npr::launch_flow_detail(ar, len, (const npr_record *)(ar + ro), n, ar + oo + so,
+                                         (uint64_t *)(ar + oo), c->stream));
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    if (status) memcpy(status, ar + oo + so, n);
+    if (detail) memcpy(detail, ar + oo, n * sizeof(uint64_t));
+    return NPR_OK;
+  }
+  st = stage_input(c, in, len);
   if (st) return st;
   if (n == 0) return NPR_OK;
   if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;

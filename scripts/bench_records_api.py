@@ -134,8 +134,8 @@ def main():
                                "Mrows_per_s": round(n / agg_ms / 1e3, 1)},
         "host_extract_flow_one_record": {"us_per_call": round(per_call_us, 1),
                                          "note": "one npr_extract_flows host call per record (the Rust "
-                                                 "FlowExtraction::extract_flow default method): H2D + launch + D2H + "
-                                                 "sync; use extract_flows / convert_records for batches"},
+                                                 "FlowExtraction::extract_flow default method): one launch over a page-locked "
+                                                 "arena + sync; use extract_flows / convert_records for batches"},
         "host_convert_records": {"ms": round(host_ms, 3), "Mrecords_per_s": round(n / host_ms / 1e3, 1),
                                  "note": "pageable host buffers: capture + records H2D, flow rows D2H"},
         "cpu_oracle_convert_records": {"ms": round(cpu_ms, 3), "Mrecords_per_s": round(n / cpu_ms / 1e3, 2),

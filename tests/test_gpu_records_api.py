@@ -169,3 +169,33 @@ def test_flow_error_details_host_call_and_mirror():
         assert e.value.code == want_st[i] and e.value.detail == int(want_det[i])
         seen += e.value.size is not None
     assert seen > 0
+
+
+@pytest.mark.parametrize("n_rec", [1, 7, 1_500, 12_000], ids=["one", "seven", "small_arena", "staged"])
+def test_host_extract_and_details_both_paths(n_rec):
+    """npr_extract_flows / npr_flow_details with host buffers: calls whose input + records fit the
+    256-KiB page-locked arena run one launch over it (the kernel reads and writes host memory);
+    larger ones stage through device buffers.  Both against the oracle, IPv6 side rows included."""
+    import net_parser_rs as npr
+    blob = synth.quirk_corpus(n_rec, seed=21)
+    recs = records_of(blob, shrink=0.2, permute=True, seed=3)
+    assert (len(blob) + 24 * len(recs) <= (256 << 10)) == (n_rec < 5_000)  # which path each case takes
+    want_f, want_v6, want_st = _oracle.extract_flows(blob, recs)
+    ctx = npr.context()
+    a = np.frombuffer(blob, dtype=np.uint8)
+    n = len(recs)
+    f = np.zeros(n, _abi.FLOW_DTYPE)
+    v6 = np.zeros(n, _abi.FLOW_V6_DTYPE)
+    st = np.zeros(n, np.uint8)
+    for _ in range(2):  # the second call reuses the arena
+        ctx.check(ctx.lib.npr_extract_flows(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, f.ctypes.data,
+                                            v6.ctypes.data, st.ctypes.data))
+        assert np.array_equal(st, want_st)
+        assert f.tobytes() == want_f.tobytes()
+        assert v6.tobytes() == want_v6.tobytes()
+    want_ds, want_det = _oracle.flow_details(blob, recs)
+    ds = np.zeros(n, np.uint8)
+    det = np.zeros(n, np.uint64)
+    ctx.check(ctx.lib.npr_flow_details(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, ds.ctypes.data,
+                                       det.ctypes.data))
+    assert np.array_equal(ds, want_ds) and np.array_equal(det, want_det)
