@@ -1407,13 +1407,33 @@ npr_status npr_convert_records(npr_ctx *c, const uint8_t *in, size_t len, const 
                                npr_flow *out, npr_flow_v6 *out_v6, size_t cap, size_t *n_out) {
   if (!c || (!in && len) || (!records && n)) return fail(c, NPR_ERR_ARG, "null argument");
   HIP_CHECK(c, hipSetDevice(c->device));
-  npr_status st = stage_input(c, in, len);
-  if (st) return st;
+  npr_status st;
   if (n == 0) {
     if (n_out) *n_out = 0;
     return NPR_OK;
   }
+  if (!small_call(len, n) && (st = stage_input(c, in, len))) return st;
   const uint64_t ocap = std::min<uint64_t>(cap, n);
+  if (small_call(len, n)) {  // one launch over the page-locked arena (rows, side rows, total)
+    uint8_t *ar = nullptr;
+    uint64_t ro = 0, oo = 0;
+    const uint64_t vo = a16(std::max<uint64_t>(ocap, 1) * sizeof(npr_flow));
+    const uint64_t to = vo + a16(std::max<uint64_t>(ocap, 1) * sizeof(npr_flow_v6));
+    if ((st = small_arena(c, in, len, records, n, to + 8, ar, ro, oo))) return st;
+    uint64_t *total = (uint64_t *)(ar + oo + to);
+    if ((st = convert_launch(c, ar, len, (const npr_record *)(ar + ro), n, (npr_flow *)(ar + oo),
+                             out_v6 ? (npr_flow_v6 *)(ar + oo + vo) : nullptr, ocap, total, c->stream)))
+      return st;
+    HIP_CHECK(c, hipStreamSynchronize(c->stream));
+    const uint64_t tot = *(volatile uint64_t *)total;
+    if (tot == ~0ull) return fail(c, NPR_ERR_TIMEOUT, "convert_records did not complete (look-back timed out)");
+    const uint64_t k = std::min<uint64_t>(tot, ocap);
+    if (k && out) memcpy(out, ar + oo, k * sizeof(npr_flow));
+    if (k && out_v6) memcpy(out_v6, ar + oo + vo, k * sizeof(npr_flow_v6));
+    if (n_out) *n_out = tot;
+    if (tot > cap) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+    return NPR_OK;
+  }
   if ((st = ensure(c, c->recs, n * sizeof(npr_record)))) return st;
   if ((st = ensure(c, c->flows2, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow)))) return st;
   if ((st = ensure(c, c->flows2_v6, std::max<uint64_t>(ocap, 1) * sizeof(npr_flow_v6)))) return st;

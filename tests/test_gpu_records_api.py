@@ -199,3 +199,18 @@ def test_host_extract_and_details_both_paths(n_rec):
     ctx.check(ctx.lib.npr_flow_details(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, ds.ctypes.data,
                                        det.ctypes.data))
     assert np.array_equal(ds, want_ds) and np.array_equal(det, want_det)
+    # convert_records over the same list (reverse LIST order), both with room for every row and capped
+    import ctypes
+    wf, wv6 = _oracle.convert_records(blob, recs)
+    for cap in (n, max(len(wf) // 2, 1)):
+        out = np.zeros(n, _abi.FLOW_DTYPE)
+        out6 = np.zeros(n, _abi.FLOW_V6_DTYPE)
+        k = ctypes.c_size_t(0)
+        rc = ctx.lib.npr_convert_records(ctx.handle, a.ctypes.data, a.size, recs.ctypes.data, n, out.ctypes.data,
+                                         out6.ctypes.data, cap, ctypes.byref(k))
+        assert k.value == len(wf)
+        assert rc == (0 if cap >= len(wf) else _abi.ERR_CAPACITY)
+        m = min(cap, len(wf))
+        assert out[:m].tobytes() == wf[:m].tobytes()
+        is6 = (wf[:m]["kind"] & _abi.KIND_IPV6) != 0
+        assert out6[:m][is6].tobytes() == wv6[:m][is6].tobytes()

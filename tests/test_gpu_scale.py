@@ -9,7 +9,7 @@
   8-GPU run holds), reconciled by the one-exchange replay and merged in reverse rank order: bit-exact
   against the oracle at 16M records, and at the full 64M;
 - C5 substitute (the 4SICS capture is absent, .MISSING_LARGE_BLOBS:1): a quirk-corpus tile
-  repeated to several GB, sharded by BYTE range with halos (speculated starts inside adversarial
+  repeated to 10 GB, sharded by BYTE range with halos (speculated starts inside adversarial
   payloads), every tile of the merged table compared with the single-tile oracle golden.
 
 The oracle (tests/_oracle.py) is the checker only.  Heavy cases print progress so a long run is
@@ -132,14 +132,14 @@ def test_c4_64m_sharded_bit_exact():
 
 
 def test_c5_tiled_quirk_capture():
-    """SURVEY.md §8 d C5 with the quirk corpus standing in for the absent 4SICS file: one tile of
-    complete records repeated to ~4 GB; byte-range shards with halos; each tile's slice of the
-    merged table equals the single-tile golden with its record offsets moved by the tile's place."""
+    """SURVEY.md §8 d C5 (10 GB) with the quirk corpus standing in for the absent 4SICS file: one
+    tile of complete records repeated to 10 GB; byte-range shards with halos; each tile's slice of
+    the merged table equals the single-tile golden with its record offsets moved by the tile's place."""
     tile_blob = synth.quirk_corpus(30_000, seed=77, fake_every=25, jumbo_every=5_000)
     hdr, recs, cons, gold, gold6 = oracle_flows(tile_blob)
     assert cons == len(tile_blob)       # a tile of complete records: the chain runs on into the next
     body = np.frombuffer(tile_blob, dtype=np.uint8)[24:]
-    T, K = body.size, 4_000_000_000 // body.size
+    T, K = body.size, 10_000_000_000 // body.size
     log(f"C5: tile {T} B x {K}")
     host = np.empty(24 + T * K, dtype=np.uint8)
     host[:24] = np.frombuffer(tile_blob[:24], dtype=np.uint8)
