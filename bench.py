@@ -293,8 +293,11 @@ def run_sharded(args, dev, local, rank, world):
     except RuntimeError as e:
         print(f"[rank {rank}] no gloo group ({e}); summaries over RCCL", file=sys.stderr, flush=True)
         meta = None
+    # four steps in flight; the oldest two are finished by ONE host exchange, so an all-gather over
+    # loopback that is slower than a parse (gloo, 8 ranks) is paid once per two parses
+    depth = 4
     step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000,
-                                       meta_group=meta)
+                                       meta_group=meta, depth=depth)
     metas, live, rounds = step.step()
     _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
     assert rounds == 1 and r_tot == n_total and f_tot == n_total, (rounds, r_tot, f_tot)
@@ -303,14 +306,14 @@ def run_sharded(args, dev, local, rank, world):
     dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # two steps in flight: step k's host replay of the exchanged summaries runs while step k+1 parses
+    # up to `depth` steps in flight: the host replay of exchanged summaries runs while later steps parse
     for _ in range(args.steps):
         step.launch_step()
-        if len(step.pending) > 1:
-            _, _, r = step.finish_step()
+        if len(step.pending) == depth:
+            _, _, r = step.finish_steps(depth // 2)
             rounds = max(rounds, r)
-    while step.pending:
-        _, _, r = step.finish_step()
+    if step.pending:
+        _, _, r = step.finish_steps(len(step.pending))
         rounds = max(rounds, r)
     torch.cuda.synchronize()
     dist.barrier()
@@ -351,8 +354,9 @@ def run_sharded(args, dev, local, rank, world):
     out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
     out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
     step_ms = wall * 1e3 / args.steps
-    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per step, "
-                                      "overlapped with the next step's parse; RCCL carries the flow rows") if meta is not None
+    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per two "
+                                      f"steps ({depth} in flight), overlapped with the later steps' parses; RCCL "
+                                      "carries the flow rows") if meta is not None
                        else "RCCL all_gather of the ranks' device summaries, one per step", "rounds": rounds}
     out["gather_ms"] = round(gather_ms, 3)
     out["gather"] = ("RCCL point-to-point of every rank's flow rows straight into rank 0's merged "

@@ -307,7 +307,7 @@ class DeviceShardedParse:
     [base, base + nbytes)."""
 
     def __init__(self, ws, buf, base, bounds, file_len, endianness=_abi.LITTLE, usec_magic=True, ts_ref=None,
-                 start=24, group=None, nbytes=None, chunk_bytes=0, meta_group=None):
+                 start=24, group=None, nbytes=None, chunk_bytes=0, meta_group=None, depth=2):
         import torch
         import torch.distributed as dist
         self.ws, self.buf, self.base, self.bounds = ws, buf, int(base), bounds
@@ -317,11 +317,13 @@ class DeviceShardedParse:
         self.chunk = int(chunk_bytes)
         self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
         self.gathered = torch.zeros(self.world * ws.summary.numel(), dtype=torch.uint8, device=ws.summary.device)
-        # launch_step / finish_step: two exchanges in flight (device + page-locked host copies)
+        # launch_step / finish_steps: up to `depth` steps in flight, each with its own exchange buffers
+        # (device + page-locked host copies)
         pin = ws.summary.device.type == "cuda"
-        self._g2 = [torch.zeros_like(self.gathered) for _ in range(2)]
-        self._h2 = [torch.zeros(self.gathered.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
-        self._ev2 = [torch.cuda.Event() if pin else None for _ in range(2)]
+        self.depth = max(2, int(depth))
+        self._g2 = [torch.zeros_like(self.gathered) for _ in range(self.depth)]
+        self._h2 = [torch.zeros(self.gathered.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(self.depth)]
+        self._ev2 = [torch.cuda.Event() if pin else None for _ in range(self.depth)]
         self._k = 0
         self.pending = []
         # meta_group (a gloo group over the same ranks): launch_step's exchange moves the 64-B
@@ -331,7 +333,7 @@ class DeviceShardedParse:
         if meta_group is not None:
             # the parse's last link stores its summary straight into page-locked host memory: the
             # host waits for an event behind the parse, no copy kernel needs a CU the next parse holds
-            self._sum2 = [torch.zeros(ws.summary.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(2)]
+            self._sum2 = [torch.zeros(ws.summary.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(self.depth)]
             self._gh = torch.zeros(self.gathered.numel(), dtype=torch.uint8)
             self._bind(self._sum2[0])
 
@@ -384,13 +386,13 @@ class DeviceShardedParse:
         """The step's device work without waiting for it: this rank's parse from its speculated (or
         known) start, the all-gather of the summaries and their copy to page-locked host memory,
         all stream-ordered.  finish_step() replays the chain on the host, so the host work of step k
-        overlaps the parse of step k+1 (at most two steps in flight: the exchange buffers alternate)."""
+        overlaps the parse of step k+1 (at most `depth` steps in flight: the exchange buffers rotate)."""
         import torch.distributed as dist
-        if len(self.pending) >= 2:
-            raise RuntimeError("finish_step() the oldest step first")
+        if len(self.pending) >= self.depth:
+            raise RuntimeError("finish_steps() the oldest steps first")
         import torch
         lo, hi = self.bounds[self.rank]
-        i = self._k & 1
+        i = self._k % self.depth
         self._k += 1
         if self.meta_group is not None:
             self._bind(self._sum2[i])
@@ -406,30 +408,50 @@ class DeviceShardedParse:
         self.pending.append(i)
 
     def finish_step(self):
-        """-> (metas, live, rounds) of the oldest launch_step().  A contradicted speculation (never on
-        C4) drains the device and runs the whole step again synchronously (every rank decides the
-        same from the same summaries, so the collectives stay matched)."""
+        """-> (metas, live, rounds) of the oldest launch_step()."""
+        return self.finish_steps(1)
+
+    def finish_steps(self, n):
+        """Finish the n oldest launch_step()s; -> (metas, live, rounds) of the last of them.  With a
+        host metadata group their summaries move in ONE all-gather (n x 64 B per rank), so a host
+        exchange slower than a parse is paid once per n steps.  Every rank must pass the same n
+        (the bench's loop decides it from len(pending), which all ranks share).  A contradicted
+        speculation (never on C4) drains the device and runs the whole step again synchronously
+        (every rank decides the same from the same summaries, so the collectives stay matched)."""
         import torch
         import torch.distributed as dist
-        i = self.pending.pop(0)
-        if self._ev2[i] is not None:
-            self._ev2[i].synchronize()
-        if self.meta_group is not None:  # the summaries' all-gather on the host (gloo)
-            dist.all_gather(list(self._h2[i].view(self.world, -1).unbind(0)), self._sum2[i], group=self.meta_group)
-        metas = self._metas(self._h2[i])
-        bad, e, live = replay(self.start, self.bounds, metas)
-        if bad is not None:
-            if torch.cuda.is_available():
-                torch.cuda.synchronize()
-            while self.pending:  # later steps parsed from the same speculation: redone below
-                self.pending.pop(0)
-            return self.step()
-        lo, hi = self.bounds[self.rank]
-        m = metas[self.rank]
-        if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
-            raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
-        self.metas, self.live = metas, live
-        return metas, live, 1
+        n = min(int(n), len(self.pending))
+        if n <= 0:
+            raise RuntimeError("no step in flight")
+        slots = [self.pending.pop(0) for _ in range(n)]
+        for i in slots:
+            if self._ev2[i] is not None:
+                self._ev2[i].synchronize()
+        if self.meta_group is not None:  # the summaries' all-gather on the host (gloo), all n steps at once
+            sn = self._sum2[0].numel()
+            mine = torch.cat([self._sum2[i] for i in slots])
+            out = torch.empty(self.world * n * sn, dtype=torch.uint8)
+            dist.all_gather(list(out.view(self.world, -1).unbind(0)), mine, group=self.meta_group)
+            per = out.view(self.world, n, sn)
+            for j, i in enumerate(slots):
+                self._h2[i].copy_(per[:, j, :].reshape(-1))
+        res = None
+        for i in slots:
+            metas = self._metas(self._h2[i])
+            bad, e, live = replay(self.start, self.bounds, metas)
+            if bad is not None:
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
+                while self.pending:  # later steps parsed from the same speculation: redone below
+                    self.pending.pop(0)
+                return self.step()
+            lo, hi = self.bounds[self.rank]
+            m = metas[self.rank]
+            if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
+                raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
+            self.metas, self.live = metas, live
+            res = (metas, live, 1)
+        return res
 
     def step(self):
         """-> (metas, live, rounds).  Raises HaloError when a chain stops short of a buffer end."""

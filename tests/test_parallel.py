@@ -225,9 +225,19 @@ def _step_rank_main(rank, world, port, blob, wrong, q, pipelined=False):
         shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
         spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
         ws = OracleShardWorkspace(len(recs) + 1, spec)
-        meta = dist.new_group(backend="gloo") if pipelined == "host_meta" else None
-        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), meta_group=meta)
-        if pipelined:  # the bench's timed loop: two steps in flight, host replay of step k during step k+1
+        meta = dist.new_group(backend="gloo") if str(pipelined).startswith("host_meta") else None
+        deep = pipelined == "host_meta_d4"
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), meta_group=meta, depth=4 if deep else 2)
+        if deep:  # the bench's N > 1 loop: four steps in flight, the oldest two finished by ONE exchange
+            rounds = 0
+            for _ in range(7):
+                step.launch_step()
+                if len(step.pending) == 4:
+                    metas, live, r = step.finish_steps(2)
+                    rounds = max(rounds, r)
+            metas, live, r = step.finish_steps(len(step.pending))
+            rounds = max(rounds, r)
+        elif pipelined:  # two steps in flight, host replay of step k during step k+1
             rounds = 0
             for _ in range(3):
                 step.launch_step()
@@ -251,7 +261,8 @@ def _step_rank_main(rank, world, port, blob, wrong, q, pipelined=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True, "host_meta"], ids=["step", "launch_finish", "host_meta"])
+@pytest.mark.parametrize("pipelined", [False, True, "host_meta", "host_meta_d4"],
+                         ids=["step", "launch_finish", "host_meta", "host_meta_depth4"])
 @pytest.mark.parametrize("wrong", [False, True], ids=["exact", "rerun"])
 def test_gloo_world2_device_step_protocol(wrong, pipelined):
     """DeviceShardedParse (the bench's multi-GPU step) + gather_flow_tables over gloo: each rank holds
