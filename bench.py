@@ -293,9 +293,9 @@ def run_sharded(args, dev, local, rank, world):
     except RuntimeError as e:
         print(f"[rank {rank}] no gloo group ({e}); summaries over RCCL", file=sys.stderr, flush=True)
         meta = None
-    # four steps in flight; the oldest two are finished by ONE host exchange, so an all-gather over
-    # loopback that is slower than a parse (gloo, 8 ranks) is paid once per two parses
-    depth = 4
+    # eight steps in flight; the oldest four are finished by ONE host exchange, so an all-gather over
+    # loopback that is slower than a parse (gloo, 8 ranks) is paid once per four parses
+    depth = 8
     step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000,
                                        meta_group=meta, depth=depth)
     metas, live, rounds = step.step()
@@ -354,8 +354,8 @@ def run_sharded(args, dev, local, rank, world):
     out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
     out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
     step_ms = wall * 1e3 / args.steps
-    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per two "
-                                      f"steps ({depth} in flight), overlapped with the later steps' parses; RCCL "
+    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per "
+                                      f"{depth // 2} steps ({depth} in flight), overlapped with the later steps' parses; RCCL "
                                       "carries the flow rows") if meta is not None
                        else "RCCL all_gather of the ranks' device summaries, one per step", "rounds": rounds}
     out["gather_ms"] = round(gather_ms, 3)
