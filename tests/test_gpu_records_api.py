@@ -123,6 +123,15 @@ def test_dev_convert_c2_full_size():
     check_dense(blob, recs)
 
 
+def test_dev_convert_beyond_64_groups():
+    """A list of more than 64 x 64 blocks of 1024 records (4.3M frames): the start rows of the upper
+    blocks fold group sums more than 64 groups below them, and a ragged last block."""
+    n = 64 * 64 * 1024 + 111_111
+    blob = synth.fixed64(n)
+    recs = records_of(blob)
+    assert check_convert(blob, recs) == n
+
+
 def dev_details(blob, recs):
     import ctypes
     import net_parser_rs as npr
