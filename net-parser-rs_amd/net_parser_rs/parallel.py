@@ -330,12 +330,31 @@ class DeviceShardedParse:
         # summaries on the HOST instead (D2H on a side stream, all-gathered in finish_step), so no
         # collective kernel or stream join sits between two parses; the flow rows still go over RCCL
         self.meta_group = meta_group
+        # every rank's buffer end, once: a chain that stops short of its shard's stop inside a buffer
+        # that does not reach the file's end is a HaloError, and every rank must decide it alike
+        # (the others would otherwise wait in their next collective for the rank that raised)
+        grp = meta_group if meta_group is not None else group
+        on_host = dist.get_backend(grp) == "gloo"
+        dev = torch.device("cpu") if on_host else ws.summary.device
+        mine = torch.tensor([self.base + self.nbytes], dtype=torch.int64, device=dev)
+        ends = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
+        dist.all_gather(ends, mine, group=grp)
+        self.buf_ends = [int(e.item()) for e in ends]
         if meta_group is not None:
             # the parse's last link stores its summary straight into page-locked host memory: the
             # host waits for an event behind the parse, no copy kernel needs a CU the next parse holds
             self._sum2 = [torch.zeros(ws.summary.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(self.depth)]
             self._gh = torch.zeros(self.gathered.numel(), dtype=torch.uint8)
             self._bind(self._sum2[0])
+
+    def _check_halo(self, metas, live):
+        """Raise HaloError on EVERY rank when any live rank's chain stopped short of its shard's stop
+        inside a buffer that ends before the file does (it needs a longer halo)."""
+        bad = [r for r in range(self.world)
+               if live[r] and metas[r].consumed < self.bounds[r][1] and self.buf_ends[r] < self.file_len]
+        if bad:
+            raise HaloError(f"ranks {bad}: a chain stopped inside a short buffer at "
+                            f"{[metas[r].consumed for r in bad]} < stop {[self.bounds[r][1] for r in bad]}")
 
     def _launch(self, start, speculative):
         lo, hi = self.bounds[self.rank]
@@ -445,16 +464,13 @@ class DeviceShardedParse:
                 while self.pending:  # later steps parsed from the same speculation: redone below
                     self.pending.pop(0)
                 return self.step()
-            lo, hi = self.bounds[self.rank]
-            m = metas[self.rank]
-            if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
-                raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
+            self._check_halo(metas, live)
             self.metas, self.live = metas, live
             res = (metas, live, 1)
         return res
 
     def step(self):
-        """-> (metas, live, rounds).  Raises HaloError when a chain stops short of a buffer end."""
+        """-> (metas, live, rounds).  Raises HaloError (on every rank) when a chain stops short of a buffer end."""
         lo, hi = self.bounds[self.rank]
         self._launch(self.start if self.rank == 0 else lo, self.rank > 0)
         rounds = 1
@@ -471,9 +487,7 @@ class DeviceShardedParse:
             else:  # keep the stream order: an empty launch is not needed, the others just re-gather
                 pass
             rounds += 1
-        m = metas[self.rank]
-        if live[self.rank] and m.consumed < hi and self.base + self.nbytes < self.file_len:
-            raise HaloError(f"rank {self.rank}: chain stopped at {m.consumed} < {hi} inside a short buffer")
+        self._check_halo(metas, live)
         self.metas, self.live = metas, live
         return metas, live, rounds
 

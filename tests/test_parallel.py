@@ -369,3 +369,45 @@ def test_gloo_world3_record_spans_a_whole_shard():
         assert p.exitcode == 0
     flows_ok, n1, rounds = q.get(timeout=10)
     assert flows_ok and n1 == 0 and rounds == 2
+
+
+# ---- a short halo: every rank raises HaloError together ------------------------------------------
+def _halo_rank_main(rank, world, port, blob, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _, recs, _, _ = full_reference(blob)
+        bounds = parallel.shard_bounds(24, len(blob), world)
+        lo, hi = bounds[rank]
+        base = 0 if rank == 0 else lo - lo % 16
+        # rank 0's buffer ends 10 bytes before its stop: the record straddling that point is cut
+        end = hi - 10 if rank == 0 else len(blob)
+        shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
+        ws = OracleShardWorkspace(len(recs) + 1, spec_exact(recs))
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
+        try:
+            step.step()
+            q.put((rank, "no error"))
+        except parallel.HaloError as e:
+            q.put((rank, "halo" if "ranks [0]" in str(e) else str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_short_halo_raises_on_every_rank():
+    """A rank whose buffer stops inside a record before its shard's stop: HaloError on BOTH ranks
+    (decided from the shared summaries and buffer ends), so no rank goes on into a collective the
+    raising rank never joins."""
+    blob = synth.fixed64(4_000)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_halo_rank_main, args=(r, 2, port, blob, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    got = sorted(q.get(timeout=10) for _ in range(2))
+    assert got == [(0, "halo"), (1, "halo")]
