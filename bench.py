@@ -52,8 +52,8 @@ def host_threads():
 
 def cpu_baseline(blob, n_records, budget_s, sample):
     """The CPU oracle (C restatement of the reference path, tests/_oracle.py), CaptureFile::parse +
-    convert_records on the same capture: on all host threads (the reported baseline) and on one
-    core (the reference itself is single-threaded, benches/benches.rs)."""
+    convert_records on the same capture: on all host threads and on one core (the reference itself
+    is single-threaded, benches/benches.rs); the faster of the two is the reported baseline."""
     import _oracle
     rec = np.zeros(n_records + 1, dtype=npr._abi.RECORD_DTYPE)
     fl = np.zeros(n_records + 1, dtype=npr._abi.FLOW_DTYPE)
@@ -76,8 +76,11 @@ def cpu_baseline(blob, n_records, budget_s, sample):
     T = host_threads()
     mt = _oracle.MtScratch(n_records + 1)
     many, pm, em = timed(lambda: _oracle.bench_extract_mt(blob, mt, T))
-    return {"value": round(many, 3), "unit": "Mpackets/s", "cores": T, "kind": "port",
-            "single_core_value": round(one, 3),
+    # the reported value is the faster of the two (the threaded run is not always faster: the serial
+    # chain walk plus a memory-bound extract), with `cores` the threads that run used
+    best_mt = many >= one
+    return {"value": round(many if best_mt else one, 3), "unit": "Mpackets/s", "cores": T if best_mt else 1,
+            "kind": "port", "threaded_value": round(many, 3), "threads": T, "single_core_value": round(one, 3),
             "sample": f"{sample} ({n_records} records, {len(blob)} B): CaptureFile::parse + convert_records "
                       f"(oracle/npr_oracle.c), {pm} passes in {em:.1f} s on {T} host threads (serial chain walk, "
                       f"parallel extract_flow); {p1} passes in {e1:.1f} s on 1 core"}
