@@ -1552,8 +1552,10 @@ __device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t
 template <uint32_t N>
 __device__ __forceinline__ uint32_t stg_slot(uint32_t c) { return (c & 1u) ? N / 2u + 8u + (c >> 1) : c >> 1; }
 
-// 16-B flow-row store.  Plain (write-back): measured 33.9 us per launch against 38.1 us with
-// write-through (sc1) stores, although the table is written in the launch's last microseconds.
+constexpr int kPolSc1 = 16;  // buffer-store cache policy: sc1 (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16)
+// 16-B flow-row store, one row per lane (the batched pass, IPv6 side rows).  Plain (write-back):
+// measured 33.9 us per launch against 38.1 us with write-through (sc1) stores in round 1's kernel,
+// which stored every row this way (phase B's row blocks are written through since round 3).
 __device__ __forceinline__ void st_wt16(uint32_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
 
 // one Ok flow row (+ its IPv6 side row, re-read from the capture at the decoded offset)
@@ -2003,7 +2005,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
                                  (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
             // The round's Ok rows are one contiguous block of nok rows: stage them in this wave's idle
             // ring slot in address order, then store the block as contiguous 16-B chunks (lane i:
-            // chunks i and 64 + i), so each store instruction writes whole lines, non-temporally.  A
+            // chunks i and 64 + i), so each store instruction writes whole lines (written through, below).  A
             // write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane
             // rounds (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s;
             // in this kernel C2 went 31.3 -> 30.8 us, and non-temporal stores a further 30.6 -> 30.1.
@@ -2024,9 +2026,13 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
               }
               wave_sync();
               u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
-              if ((uint32_t)lane < 2u * nok) __builtin_nontemporal_store(stg[stg_slot<128>(lane)], dst + lane);
-              if ((uint32_t)lane + 64u < 2u * nok)
-                __builtin_nontemporal_store(stg[stg_slot<128>(lane + 64)], dst + lane + 64);
+              // write-through (sc1) stores through a buffer resource over exactly the block (its range
+              // check drops the chunks past 2 nok): no dirty lines left in the XCD's L2 for the kernel-
+              // end write-back.  Interleaved A/B on one box (scripts/gpu_variants.sh, round 3): C2
+              // 28.1-28.5 us against 30.3-30.7 us non-temporal, C3 1.443 against 1.478 ms
+              const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, (int)(2u * nok * 16u), 0x00020000);
+              __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane)], rr, (int)(lane * 16u), 0, kPolSc1);
+              __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane + 64)], rr, (int)((lane + 64u) * 16u), 0, kPolSc1);
               if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
               wave_sync();  // the slot is rewritten by the next round
             } else if ((bal >> lane) & 1ull) {
@@ -2294,7 +2300,9 @@ __global__ __launch_bounds__(kBlock) void k_extract_dense(const uint8_t *buf, ui
     stg[stg_slot<2 * kBlock>(2 * threadIdx.x)] = t == 0 ? r0 : s0;
     stg[stg_slot<2 * kBlock>(2 * threadIdx.x + 1)] = t == 0 ? r1 : s1;
     __syncthreads();
-    // non-temporal (streaming) stores, as phase B's row blocks: 23.9 -> 23.4 us per 1M C2 records
+    // non-temporal (streaming) stores: 23.9 -> 23.4 us per 1M C2 records.  Write-through (sc1, or
+    // sc0 sc1), which phase B's row blocks use since round 3, measured the same here: 23.3-23.9 us
+    // for all three policies (profiles/r03_block_store_policy_ab.json)
     uint4 *dst = reinterpret_cast<uint4 *>(out + b0 * 8);
     if (threadIdx.x < nch) st_nt16(dst + threadIdx.x, stg + stg_slot<2 * kBlock>(threadIdx.x));
     if (threadIdx.x + kBlock < nch)
