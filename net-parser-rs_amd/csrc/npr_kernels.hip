@@ -1686,7 +1686,8 @@ __device__ __forceinline__ uint32_t res_stage(const StageParams &q, ResShared &w
 //   kResRing tiles of its range of the next capture in its idle ring (the read that the look-back and the
 //   row writes would otherwise leave HBM without), so `next` starts with them landed; `staged`
 //   says this capture's tiles were staged that way, with its speculation bytes in scb.  The rows
-//   go out one per lane (the ring slot the single-capture pass stages row blocks in holds the next capture).
+//   go out in 32-row blocks staged in the wave's record-offset scratch (the ring slot the
+//   single-capture pass stages row blocks in holds the next capture).
 // Returns false when the workgroup must leave the kernel (a bounded wait timed out).
 template <bool DIAG, bool PACK, bool BATCH>
 __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &sh, bool has_next, StageParams nx,
@@ -2009,10 +2010,36 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
             // write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane
             // rounds (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s;
             // in this kernel C2 went 31.3 -> 30.8 us, and non-temporal stores a further 30.6 -> 30.1.
-            // (BATCH: the ring holds the next capture's tiles: one row per lane.)
+            // (BATCH: the ring holds the next capture's tiles: 32-row halves through srec, below.)
             const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
             const uint64_t f0 = xo + okb;
-            if (!BATCH && nok && f0 + nok <= kp.flow_cap) {
+            if (BATCH && nok && f0 + nok <= kp.flow_cap) {
+              // the ring holds the next capture's tiles: the block goes out 32 rows at a time, staged
+              // in this wave's record-offset scratch (1 KiB, dead until the next walk; chunk c at slot
+              // c: the row stores are 2-way bank-conflicted, which the ring's stg_slot layout avoids)
+              const bool mine = (bal >> lane) & 1ull;
+              const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+              const uint64_t p = base + fl[q][7];
+              const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+              const uint32_t k = nok - 1u - rank;
+              u32x4 *stg = reinterpret_cast<u32x4 *>(sh.w[wid].srec);
+              static_assert(sizeof(sh.w[0].srec) >= 64 * 16, "32 rows fit the record-offset scratch");
+              u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
+              for (uint32_t h = 0; h < nok; h += 32u) {
+                if (mine && k >= h && k < h + 32u) {
+                  stg[2u * (k - h)] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
+                  stg[2u * (k - h) + 1u] =
+                      u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+                }
+                wave_sync();
+                const uint32_t nh = nok - h < 32u ? nok - h : 32u;
+                const __amdgpu_buffer_rsrc_t rr =
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(dst + 2u * h), 0, (int)(2u * nh * 16u), 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(stg[lane], rr, (int)(lane * 16u), 0, kPolSc1);
+                wave_sync();  // the scratch is rewritten by the next half
+              }
+              if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
+            } else if (!BATCH && nok && f0 + nok <= kp.flow_cap) {
               const bool mine = (bal >> lane) & 1ull;
               const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
               const uint64_t p = base + fl[q][7];
