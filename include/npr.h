@@ -250,13 +250,21 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   memory.  Same results as the staged call, except that a record longer than the halo cannot
  *   cross a chunk end in the window: the call then returns NPR_ERR_CAPACITY (a pcap snaplen is at
  *   most 262144 B, which the halo covers).  Windowed chunks are at least 512 KiB.
+ * NPR_OPT_SPARSE (default 0 = auto): flows-only parses of captures of long records run the sparse
+ *   record walk instead of the resident pass: lanes hop header to header and read
+ *   one 112-B window per record instead of streaming every payload byte.  0 chooses it from the
+ *   record density of the capture's first 256 KiB (at least 16 MiB past `start`, a known start, no
+ *   shard); 1 never; 2 always (lane ranges sized from the density, else 16 KiB); N >= 64 always,
+ *   with lane ranges of N bytes (a test knob).  Same results either way.
+ * NPR_OPT_SPARSE_CAP (default 0 = 64): Ok-flow slots per sparse lane; a lane with more Ok flows
+ *   walks the rest again when its rows are written (a test knob; 1 .. 4096).
  */
 enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4,
-       NPR_OPT_DEVICE_WINDOW = 5 };
+       NPR_OPT_DEVICE_WINDOW = 5, NPR_OPT_SPARSE = 6, NPR_OPT_SPARSE_CAP = 7 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Which pass the context's last device parse launch ran (tests and diagnostics; no reference
  * counterpart): 0 none yet, 1 the two-pass kernels, 2 the resident single pass, 4 a batched
- * resident launch. */
+ * resident launch, 8 the sparse record walk. */
 int npr_ctx_last_pass(const npr_ctx *ctx);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);

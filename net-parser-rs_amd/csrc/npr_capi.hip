@@ -63,6 +63,21 @@ struct npr_ctx {
   // ... through a bounded device window (NPR_OPT_DEVICE_WINDOW): chunk ring + flow-row ring
   int window = 0;                        // chunks (0 = auto: only when the staged capture would not fit)
   std::vector<hipEvent_t> row_copied;    // D2H of a flow-ring slot done (the slot may be rewritten)
+  // the sparse record walk (npr_sparse.hip): NPR_OPT_SPARSE / NPR_OPT_SPARSE_CAP, the lane-range bytes
+  // this call's flows-only launches use (0 = the resident pass), its workspace
+  int sparse_mode = 0;
+  uint32_t sparse_cap = 0;
+  uint64_t sparse_span = 0;
+  DevBuf sparse;
+  // record density of recently probed captures (device pointer, range, byte order -> bytes per
+  // record): the choice of pass never changes a result, so a stale entry only costs time
+  struct Probe {
+    const void *input = nullptr;
+    uint64_t start = 0, stop = 0, mean = 0;
+    int e = -1;
+  };
+  Probe probes[8];
+  uint32_t probe_next = 0;
   std::string err;
 };
 
@@ -114,7 +129,7 @@ npr_status ensure(npr_ctx *c, DevBuf &b, size_t bytes, bool zero = false) {
 static npr_status next_epoch(npr_ctx *c, hipStream_t s) {
   if (++c->epoch > 0xffffu) {
     c->epoch = 1;
-    HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
+    if (c->slots.p) HIP_CHECK(c, hipMemsetAsync(c->slots.p, 0, c->slots.cap, s));
     HIP_CHECK(c, hipMemsetAsync(c->abort_word, 0, kCtlBytes, s));
   }
   return NPR_OK;
@@ -151,6 +166,74 @@ uint64_t tiles_for(uint64_t len, uint64_t start, uint64_t *org_out) {
 }
 
 hipStream_t pick(npr_ctx *c, void *stream) { return stream ? (hipStream_t)stream : c->stream; }
+
+// ---- which flows-only pass: the record density of a device capture ----------------------------
+constexpr uint64_t kProbeBytes = 256u << 10;        // walked from the known first record
+constexpr uint64_t kSparseMinBytes = 16ull << 20;   // auto: the sparse walk for ranges from this size on
+constexpr uint64_t kSparseMinMean = 384;            // ... of at least this many bytes per record (16 + incl)
+constexpr uint64_t kSparseSpanDefault = 16u << 10;  // lane range when the density is unknown
+constexpr uint64_t kSparseSpanRecords = 24;         // lane range = this many mean records
+// Records from the exact record start `start` in the capture's first kProbeBytes: *n and their
+// bytes per record (header included), 0 when fewer than 16 fit.  One pinned D2H copy and a sync,
+// remembered per capture (the choice of pass never changes a result: a stale entry costs time only).
+npr_status probe_density(npr_ctx *c, const void *input, uint64_t start, uint64_t stop, npr_endianness e,
+                         void *stream, uint64_t &mean, uint64_t &n) {
+  for (const auto &pr : c->probes)
+    if (pr.input == input && pr.start == start && pr.stop == stop && pr.e == (int)e) {
+      mean = pr.mean;
+      n = pr.mean ? 16 : 0;
+      return NPR_OK;
+    }
+  const uint64_t nb = std::min<uint64_t>(stop - start, kProbeBytes);
+  if (!c->head_h) HIP_CHECK(c, hipHostMalloc((void **)&c->head_h, kProbeBytes, 0));
+  hipStream_t s = pick(c, stream);
+  HIP_CHECK(c, hipMemcpyAsync(c->head_h, (const uint8_t *)input + start, nb, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(c, hipStreamSynchronize(s));
+  uint64_t off = 0;
+  n = 0;
+  while (off + 16 <= nb) {
+    const uint32_t incl = rd_u32(c->head_h + off + 8, e == NPR_BIG);
+    if (off + 16 + incl > nb) break;
+    off += 16 + (uint64_t)incl;
+    ++n;
+  }
+  mean = n >= 16 ? off / n : 0;
+  npr_ctx::Probe &pr = c->probes[c->probe_next++ % 8];
+  pr.input = input;
+  pr.start = start;
+  pr.stop = stop;
+  pr.e = (int)e;
+  pr.mean = mean;
+  return NPR_OK;
+}
+bool sparse_forced(const npr_ctx *c) { return c->sparse_mode == 2 || c->sparse_mode >= 64; }
+// Lane-range bytes of the sparse record walk for a flows-only parse of records starting in
+// [start, stop), 0 = the resident pass.  known: `start` is an exact record start of a capture that
+// `input` holds from byte 0 (not a shard, not a speculative start), so its density can be probed.
+npr_status sparse_choice(npr_ctx *c, const void *input, uint64_t start, uint64_t stop, npr_endianness e, bool known,
+                         void *stream, uint64_t &span) {
+  span = 0;
+  const int m = c->sparse_mode;
+  if (m == 1) return NPR_OK;
+  if (m >= 64) {
+    span = (uint64_t)m;
+    return NPR_OK;
+  }
+  if (m == 0 && (!known || stop <= start || stop - start < kSparseMinBytes)) return NPR_OK;
+  uint64_t mean = 0, n = 0;
+  if (known && stop > start) {
+    const npr_status st = probe_density(c, input, start, stop, e, stream, mean, n);
+    if (st) return st;
+  }
+  const uint64_t sized = std::min<uint64_t>(std::max<uint64_t>(kSparseSpanRecords * mean, 4u << 10), 1u << 20);
+  if (m == 2) span = mean ? sized : kSparseSpanDefault;
+  else if (mean >= kSparseMinMean) span = sized;
+  return NPR_OK;
+}
+struct SpanScope {  // this call's flows-only launches run the sparse walk; later calls choose again
+  npr_ctx *c;
+  ~SpanScope() { c->sparse_span = 0; }
+};
 
 // ---- launch order across contexts ------------------------------------------------------------
 // The look-back kernels (k_parse_resident, the two-pass folds, k_convert_records) have workgroups
@@ -288,7 +371,7 @@ void npr_ctx_destroy(npr_ctx *c) {
     }
   }
   for (DevBuf *b : {&c->slots, &c->srec, &c->stamps, &c->chain, &c->in, &c->recs, &c->status, &c->flows, &c->flows_v6, &c->flows2,
-                    &c->flows2_v6, &c->agg})
+                    &c->flows2_v6, &c->agg, &c->sparse})
     if (b->p) (void)hipFree(b->p);
   if (c->abort_word) (void)hipFree(c->abort_word);
   if (c->summary) (void)hipFree(c->summary);
@@ -326,6 +409,14 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
     case NPR_OPT_DEVICE_WINDOW:  // chunks of the capture on the device at once (0 = auto)
       if (value < 0 || value == 1 || value == 2) return fail(c, NPR_ERR_ARG, "NPR_OPT_DEVICE_WINDOW: 0 (auto) or >= 3 chunks");
       c->window = value;
+      return NPR_OK;
+    case NPR_OPT_SPARSE:  // 0 auto (record density), 1 never, 2 always, N >= 64: always, lane ranges of N bytes
+      if (value < 0 || (value > 2 && value < 64)) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE: 0, 1, 2 or >= 64 bytes");
+      c->sparse_mode = value;
+      return NPR_OK;
+    case NPR_OPT_SPARSE_CAP:  // Ok-flow slots per lane (0 = the default)
+      if (value < 0 || value > 4096) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE_CAP: 0 .. 4096");
+      c->sparse_cap = (uint32_t)value;
       return NPR_OK;
     case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first
       if (value < 0 || (value > 0 && value < 64)) return fail(c, NPR_ERR_ARG, "NPR_OPT_STREAM_CHUNK: 0 or >= 64 KiB");
@@ -412,9 +503,17 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                  npr_endianness e, const npr_dev_outputs *o, void *stream) {
   // flows-only captures larger than one launch keeps in registers: chained chunks of that size
-  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start) {
+  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start && input &&
+      ((uintptr_t)input & 15u) == 0) {
     npr_status st = res_geometry(c);
     if (st) return st;
+    uint64_t span = 0;  // long records: the sparse walk, one launch set for any size
+    if ((st = sparse_choice(c, input, start, len, e, true, stream, span))) return st;
+    if (span) {
+      SpanScope scope{c};
+      c->sparse_span = span;
+      return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
+    }
     if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
       return npr_dev_parse_extract_chunked(c, input, len, start, e, o, 0, stream);
   }
@@ -482,6 +581,13 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
     return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream, sh);
   npr_status st = res_geometry(c);
   if (st) return st;
+  uint64_t span = 0;  // long records: sparse links (chunk_bytes 0: one sparse launch set for the range)
+  if ((st = sparse_choice(c, input, start, stop, e, !speculative_start && !sh, stream, span))) return st;
+  SpanScope span_scope{c};
+  if (span) {
+    c->sparse_span = span;
+    if (!chunk_bytes) return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream, sh);
+  }
   uint64_t chunk = chunk_bytes;
   // the waves one link runs (NPR_OPT_RESIDENT N > 1 caps them, as launch_range does)
   const uint64_t waves = c->resident > 1 ? std::min<uint64_t>(c->res_waves, (uint64_t)c->resident) : c->res_waves;
@@ -492,22 +598,10 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
     if (stop - start >= 8 * dense && !speculative_start && !sh) {
       // large: size the links by the record density of the capture's first 256 KiB, walked here from
       // the known first record (one small D2H copy and a sync; results never depend on it)
-      constexpr uint64_t kHead = 256u << 10;
-      const uint64_t nb = std::min<uint64_t>(stop - start, kHead);
-      if (!c->head_h) HIP_CHECK(c, hipHostMalloc((void **)&c->head_h, kHead, 0));
-      const uint8_t *head = c->head_h;
-      hipStream_t s = pick(c, stream);
-      HIP_CHECK(c, hipMemcpyAsync(c->head_h, (const uint8_t *)input + start, nb, hipMemcpyDeviceToHost, s));
-      HIP_CHECK(c, hipStreamSynchronize(s));
-      uint64_t off = 0, n = 0;
-      while (off + 16 <= nb) {
-        const uint32_t incl = rd_u32(head + off + 8, e == NPR_BIG);
-        if (off + 16 + incl > nb) break;
-        off += 16 + (uint64_t)incl;
-        ++n;
-      }
-      if (n >= 64) {  // 3/4 of the kept capacity at that many bytes per record
-        const uint64_t fit = waves * npr::kResSlots * 64 * 7 / 8 * (off / n);
+      uint64_t mean = 0, n = 0;
+      if ((st = probe_density(c, input, start, stop, e, stream, mean, n))) return st;
+      if (mean) {  // 7/8 of the kept capacity at that many bytes per record
+        const uint64_t fit = waves * npr::kResSlots * 64 * 7 / 8 * mean;
         chunk = std::max(dense, fit);
       }
       pack = chunk > dense;  // links past one kept round per tile: sparse tiles must share rounds
@@ -581,6 +675,54 @@ static npr_status range_params(npr_ctx *c, const void *input, uint64_t len, uint
   return NPR_OK;
 }
 
+// The sparse record walk (npr_sparse.hip) over records starting in [p.start, p.stop): lane ranges
+// of `span` bytes, 64 per group; its workspace: lanes | group aggregates | first entries | group
+// prefixes | control word | Ok-flow slots (flows requested only).
+static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summary *prev, const npr_dev_outputs *o,
+                                hipStream_t s, uint64_t span) {
+  npr::SparseParams sp{};
+  const uint64_t range = p.stop > p.start ? p.stop - p.start : 0;
+  sp.span = span;
+  sp.nlanes = (range + span - 1) / span;
+  const uint64_t ng = (sp.nlanes + 63) / 64;
+  if (ng > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large for the sparse walk");
+  sp.ngroups = (uint32_t)ng;
+  sp.cap = c->sparse_cap ? c->sparse_cap : npr::kSparseCapDefault;
+  auto a256 = [](uint64_t x) { return (x + 255) & ~255ull; };
+  const uint64_t o_agg = a256(sp.nlanes * sizeof(npr::SparseLane)), o_first = o_agg + a256(ng * npr::kSparseAggWords * 8),
+                 o_pre = o_first + a256(ng * 8), o_scan = o_pre + a256(ng * sizeof(npr::SparsePre)),
+                 o_ctl = o_scan + a256(npr::sparse_scan_words(ng) * 8), o_area = o_ctl + 256,
+                 total = o_area + (o->flows ? ng * sp.cap * 64 * 32 : 0);
+  npr_status st = ensure(c, c->sparse, total);
+  if (st) return st;
+  char *b = (char *)c->sparse.p;
+  sp.lanes = (npr::SparseLane *)b;
+  sp.aggs = (uint64_t *)(b + o_agg);
+  sp.first_entry = (uint64_t *)(b + o_first);
+  sp.pre = (npr::SparsePre *)(b + o_pre);
+  sp.scan = (uint64_t *)(b + o_scan);
+  sp.ctl = (uint64_t *)(b + o_ctl);
+  sp.area = o->flows ? (uint32_t *)(b + o_area) : nullptr;
+  if ((st = next_epoch(c, s))) return st;
+  p.epoch = c->epoch;
+  p.timeout_ticks = kTimeoutTicks;
+  p.abort_word = c->abort_word;
+  p.flows = (uint32_t *)o->flows;
+  p.flows_v6 = (uint32_t *)o->flows_v6;
+  p.flow_cap = o->flow_cap;
+  p.summary = o->summary;
+  p.stats = c->stats;
+  if (prev) {
+    p.prev = prev;
+    p.prev_epoch = summary_epoch(c, prev);
+  }
+  sp.kp = p;
+  if ((st = ordered_launch(c, s, [&] { return npr::launch_sparse(sp, s); }))) return st;
+  c->last_pass = 8;
+  log_summary(c, o->summary);
+  return NPR_OK;
+}
+
 static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start, uint64_t stop,
                                npr_endianness e, int speculative_start, uint64_t ref_record,
                                const npr_summary *prev, const npr_dev_outputs *o, void *stream,
@@ -596,6 +738,12 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
   uint64_t nt = 0;
   npr_status st = range_params(c, input, len, start, stop, e, speculative_start, ref_record, sh, p, nt);
   if (st) return st;
+  const bool flows_only = !o->record_offsets && !o->records && !o->record_status;
+  if (c->resident && flows_only && (c->sparse_span || sparse_forced(c))) {
+    const uint64_t span = c->sparse_span ? c->sparse_span : (c->sparse_mode >= 64 ? (uint64_t)c->sparse_mode : kSparseSpanDefault);
+    if (prev && speculative_start) return fail(c, NPR_ERR_ARG, "a chained launch continues an exact chain");
+    return sparse_launch(c, p, prev, o, pick(c, stream), span);
+  }
   if ((st = ensure(c, c->slots, slot_bytes(nt), true))) return st;
   if ((st = ensure(c, c->srec, nt * npr::kMaxRec * sizeof(uint16_t), false))) return st;
   hipStream_t s = pick(c, stream);
@@ -683,6 +831,7 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
 static bool batch_eligible(npr_ctx *c, const npr_batch_item &it) {
   const npr_dev_outputs &o = it.out;
   if (!c->resident || o.record_offsets || o.records || o.record_status || !o.summary) return false;
+  if (sparse_forced(c)) return false;  // every flows-only launch runs the sparse walk
   if (!it.input || it.len <= it.start || ((uintptr_t)it.input & 15u)) return false;
   if (o.flows && (((uintptr_t)o.flows & 15u) || (o.flows_v6 && ((uintptr_t)o.flows_v6 & 15u)))) return false;
   if (it.len >= (1ull << 40)) return false;

@@ -167,4 +167,39 @@ hipError_t launch_convert_records(const uint8_t *buf, uint64_t len, const npr_re
                                   uint64_t *total, uint64_t timeout_ticks, hipStream_t s);
 uint64_t convert_look_words(uint64_t n);
 
+// ---- the sparse record walk (npr_sparse.hip): flows-only parses of captures of
+// long records.  The range [start, stop) is cut into lane ranges of `span` bytes; each lane
+// speculates its first record, hops header to header with direct loads (never streaming the
+// payloads), decodes each record from one window, and keeps its Ok flows in `cap` slots.  A scan
+// kernel makes the lanes' chains exact (re-walking mis-speculated lanes) and a row kernel moves
+// the slots to their convert_records rows.
+struct SparseLane {  // one lane range's walk (k_sparse_walk; rewritten exact by a k_sparse_scan fix-up)
+  uint64_t entry;    // first record (speculated, or exact), ~0 = none found
+  uint64_t exit;     // chain position after the range, or the incomplete record (chain END)
+  uint32_t cnt, ok;  // records / Ok flows
+  uint64_t ovf;      // the first record whose Ok flow has no slot (~0: every Ok flow has one)
+};
+struct SparsePre {   // exact chain state before a 64-lane group (k_sparse_scan -> k_sparse_rows)
+  uint64_t exit, cnt, ok, pad;
+};
+constexpr uint32_t kSparseAggWords = 8;  // a 64-lane group's aggregate (npr::Seg, 64 B)
+struct SparseParams {
+  ParseParams kp;         // buf, len, start, stop, ref, big, epoch, frac_max, flags, ts_ref, flows,
+                          // flows_v6, flow_cap, summary, prev, prev_epoch, stats (the rest unused)
+  uint64_t span;          // bytes per lane range (lane i: [start + i span, min(+span, stop)))
+  uint64_t nlanes;
+  uint32_t ngroups;       // ceil(nlanes / 64): one wave of k_sparse_walk each
+  uint32_t cap;           // Ok-flow slots per lane
+  SparseLane *lanes;      // [nlanes]
+  uint64_t *aggs;         // [ngroups][kSparseAggWords]
+  uint64_t *first_entry;  // [ngroups]: the group's first lane entry found (speculative starts)
+  SparsePre *pre;         // [ngroups]
+  uint64_t *ctl;          // [0] = {epoch, 1} once the scan finished exact (the row kernel checks it)
+  uint32_t *area;         // [ngroups][cap][64] rows of 8 words (Ok flows in row image, IPv6: word 0 = v6 offset)
+  uint64_t *scan;         // k_sparse_scan's scratch: sparse_scan_words(ngroups) words
+};
+constexpr uint64_t sparse_scan_words(uint64_t ngroups) { return 7 * ngroups + 2; }
+hipError_t launch_sparse(const SparseParams &sp, hipStream_t s);
+constexpr uint32_t kSparseCapDefault = 64;
+
 }  // namespace npr

@@ -1,0 +1,812 @@
+// npr_sparse.hip — the SPARSE record walk: flows-only parses of captures whose
+// records are long (SURVEY.md §8 d, C3: 16 + min(incl, 64) bytes of a ~800-B record are all the
+// path needs).  It replaces, on the device, the same reference paths as the resident pass:
+//   PcapRecords::parse loop        src/record.rs:21-54   (offset_{k+1} = offset_k + 16 + incl_len_k)
+//   PcapRecord::parse              src/record.rs:102-121
+//   FlowExtraction::extract_flow   src/flow/mod.rs:20-48 (decode_fast / decode<>)
+//   flow::convert_records          src/flow/mod.rs:101-123 (reverse-order rows of the Ok flows)
+// without streaming the payloads through the chip:
+//   k_sparse_walk  [start, stop) is cut into lane ranges of `span` bytes, one per LANE.  A lane
+//     speculates its first record (a zero-byte mask over 112-B windows screens every byte offset
+//     for the high bytes of incl_len / orig_len, survivors are checked on their header and two
+//     chained headers), then hops header to header: each record is ONE 112-B window (the header
+//     and the decoder's bytes) loaded straight into registers, the next record's window in flight
+//     while this one decodes.  Ok flows go to the lane's slots; each 64-lane group (one wave)
+//     publishes its aggregate under the chain-consistency monoid.
+//   k_sparse_scan  one workgroup scans the group aggregates from the anchor (start, or the previous
+//     link's summary).  Groups whose speculation is contradicted are resolved lane by lane from
+//     their incoming chain position (lanes a record spans are marked passed over, mis-speculated
+//     lanes re-walked exactly) and the scan repeats until every link is exact; then it writes each
+//     group's exact prefix and the summary.
+//   k_sparse_rows  one workgroup per group moves its lanes' slots to their convert_records rows
+//     (destination order: whole-line stores); a lane with more Ok flows than slots walks the rest
+//     again from its first slotless record.
+// A wrong speculation costs a re-walk, never a result: the summary and rows are the serial chain's.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "npr_decode.hpp"
+#include "npr_device.hpp"
+#include "npr_internal.hpp"
+
+namespace npr {
+namespace {
+
+constexpr int kSpBlock = 256;                // walk / rows kernels: four 64-lane groups per workgroup
+constexpr int kSpWin = 112;                  // bytes loaded per record: [header & ~15, +112)
+constexpr int kSpRow = kSpWin / 4 + 1;       // a lane's LDS row (odd dword stride: conflict-free)
+constexpr int kScanThreads = 1024;           // k_sparse_scan: one workgroup
+constexpr int kResolvers = 256;              // groups resolved per scan round
+static_assert(15 + 16 + 18 * 4 <= kSpWin, "header + decode_fast's 18-word window fit the row at any misalignment");
+
+typedef const __attribute__((address_space(1))) u32x4 *gv4_t;  // global (not flat) loads: vmcnt only
+struct SpWin {
+  u32x4 v[kSpWin / 16];
+};
+
+__device__ __forceinline__ const uint8_t *align16(const uint8_t *p) {
+  return (const uint8_t *)((uintptr_t)p & ~(uintptr_t)15);
+}
+__device__ __noinline__ uint32_t tail_dword(const uint8_t *p, const uint8_t *end) {
+  uint32_t x = 0;
+  for (int b = 0; b < 4; ++b)
+    if (p + b < end) x |= (uint32_t)p[b] << (8 * b);
+  return x;
+}
+// a 4-aligned dword of the input, bytes at or past `end` read as 0
+__device__ __forceinline__ uint32_t dword_at(const uint8_t *p, const uint8_t *end) {
+  return p + 4 <= end ? *reinterpret_cast<const uint32_t *>(p) : (p < end ? tail_dword(p, end) : 0u);
+}
+// the window [a16, a16 + 112) into registers (seven dwordx4 issued back to back); the last bytes
+// of the buffer dword by dword
+__device__ __forceinline__ void win_load(const uint8_t *a16, const uint8_t *end, SpWin &W) {
+  if (a16 + kSpWin <= end) {
+    const gv4_t s = (gv4_t)(uintptr_t)a16;
+#pragma unroll
+    for (int k = 0; k < kSpWin / 16; ++k) W.v[k] = s[k];
+  } else {
+#pragma unroll
+    for (int k = 0; k < kSpWin / 16; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) W.v[k][e] = dword_at(a16 + 16 * k + 4 * e, end);
+  }
+}
+__device__ __forceinline__ void win_store(const SpWin &W, uint32_t *row) {
+#pragma unroll
+  for (int k = 0; k < kSpWin / 16; ++k)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) row[4 * k + e] = W.v[k][e];
+}
+
+// payload reader over a lane's staged window, global bytes (bounds-checked) past it
+struct SpRowReader {
+  const uint32_t *w;  // the lane's LDS row
+  uint32_t rel;       // payload start inside the row
+  const uint8_t *g;   // payload start in global memory
+  uint64_t gavail;    // bytes of the input from the payload start
+  __device__ __forceinline__ uint32_t le32(uint32_t q) const {
+    const uint64_t a = (uint64_t)rel + q;
+    if (a + 4 <= (uint64_t)kSpWin) return lds_le32(w, (uint32_t)a);
+    return u8g(q) | (u8g(q + 1) << 8) | (u8g(q + 2) << 16) | (u8g(q + 3) << 24);
+  }
+  __device__ __forceinline__ uint32_t u8(uint32_t q) const {
+    const uint64_t a = (uint64_t)rel + q;
+    if (a < (uint64_t)kSpWin) return ((const uint8_t *)w)[a];
+    return u8g(q);
+  }
+  __device__ __forceinline__ uint32_t u8g(uint32_t q) const { return (uint64_t)q < gavail ? g[q] : 0u; }
+};
+
+// ---- lane geometry and the monoid over lanes --------------------------------------------------
+__device__ __forceinline__ uint64_t lane_lo(const SparseParams &sp, uint64_t i) { return sp.kp.start + i * sp.span; }
+__device__ __forceinline__ uint64_t sp_end(const SparseParams &sp, int64_t i) {  // end of lane i (i = -1: start)
+  const uint64_t e = sp.kp.start + (uint64_t)(i + 1) * sp.span;
+  return e < sp.kp.stop ? e : sp.kp.stop;
+}
+
+// X then Y (Y's lanes follow X's), the chain-consistency monoid of the resident pass (combine())
+// over lane ranges.  A contradicted link records the lowest mis-speculated lane and then carries
+// Y's speculated exit on (the scan resolves contradictions group by group, each from the chain
+// position the groups before it deliver, so the propagation must not stop at the first one).
+__device__ __forceinline__ Seg sp_cat(const SparseParams &sp, const Seg &X, const Seg &Y) {
+  Seg r = X;
+  r.last = Y.last;
+  if (X.exit < sp_end(sp, X.last)) return r;   // the chain ended inside X (Q3): Y is moot
+  if (X.exit >= sp_end(sp, Y.last)) return r;  // one record spans all of Y: no record starts there
+  const bool bad = X.exit != Y.entry;
+  r.exit = Y.exit;
+  r.cnt = X.cnt + Y.cnt;
+  r.ok = X.ok + Y.ok;
+  if (X.valid && (bad || !Y.valid)) {
+    r.valid = 0;
+    r.mism = bad ? Y.first : Y.mism;
+  }
+  return r;
+}
+// lane li's segment (a lane without a speculated start: its range end as the exit guess)
+__device__ __forceinline__ Seg lane_seg(const SparseParams &sp, uint64_t li, const SparseLane &L) {
+  Seg s;
+  s.entry = L.entry;
+  s.exit = L.entry == kNone ? sp_end(sp, (int64_t)li) : L.exit;
+  s.cnt = L.cnt;
+  s.ok = L.ok;
+  s.first = s.last = (int64_t)li;
+  s.mism = -1;
+  s.valid = 1;
+  s.spare = 0;
+  return s;
+}
+__device__ __forceinline__ void put_seg(uint64_t *d, const Seg &s) {
+  d[0] = s.entry;
+  d[1] = s.exit;
+  d[2] = s.cnt;
+  d[3] = s.ok;
+  d[4] = (uint64_t)s.first;
+  d[5] = (uint64_t)s.last;
+  d[6] = (uint64_t)s.mism;
+  d[7] = s.valid;
+}
+__device__ __forceinline__ Seg get_seg(const uint64_t *d) {
+  Seg s;
+  s.entry = d[0];
+  s.exit = d[1];
+  s.cnt = d[2];
+  s.ok = d[3];
+  s.first = (int64_t)d[4];
+  s.last = (int64_t)d[5];
+  s.mism = (int64_t)d[6];
+  s.valid = (uint32_t)d[7];
+  s.spare = 0;
+  return s;
+}
+
+// ---- speculation ------------------------------------------------------------------------------
+// bit i: byte i of d is zero
+__device__ __forceinline__ uint32_t zmask4(uint32_t d) {
+  const uint32_t z = ~(((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d | 0x7F7F7F7Fu);
+  return ((z >> 7) * 0x01020408u) >> 24;
+}
+// the 16-B record header at file offset q (any alignment) in the capture's byte order
+__device__ __forceinline__ void hdr_at(const ParseParams &kp, uint64_t q, uint32_t (&h)[4]) {
+  const uint8_t *end = kp.buf + kp.len, *p = kp.buf + q;
+  const uint8_t *a4 = (const uint8_t *)((uintptr_t)p & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+  uint32_t x[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) x[k] = dword_at(a4 + 4 * k, end);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t v = __builtin_amdgcn_alignbyte(x[k + 1], x[k], sh);
+    h[k] = kp.big ? __builtin_bswap32(v) : v;
+  }
+}
+// Does the chain from a candidate (its header: ts, incl at q0) go on plausibly for two more
+// headers?  Headers past the input (an exact end, a truncated tail) cannot be checked and pass
+// (chain_grade()'s "weak" starts).  A heuristic only: the scan verifies every start exactly.
+__device__ bool chain_ok(const ParseParams &kp, const SpecCtx &sc, uint64_t q0, uint32_t ts, uint32_t incl) {
+  uint64_t q = q0 + 16 + incl;
+  for (int hop = 0; hop < 2; ++hop) {
+    if (q >= kp.len || kp.len - q < 16) return true;
+    uint32_t h[4];
+    hdr_at(kp, q, h);
+    if (!plaus(sc, h[0], h[1], h[2], h[3]) || h[0] - ts + kTsWindow > 2u * kTsWindow) return false;
+    if (kp.len - q - 16 < h[2]) return true;
+    ts = h[0];
+    q += 16 + (uint64_t)h[2];
+  }
+  return true;
+}
+// The first plausible record start in [lo, hi), kNone if none.  Windows of 96 candidate offsets:
+// every candidate needs the high bytes of incl_len and orig_len zero (both <= 2^18), which one
+// zero-byte mask over the window screens at once; the survivors are checked on their own header
+// (plaus(), the payload fits) and their chain (chain_ok()), in offset order.
+__device__ uint64_t lane_speculate(const ParseParams &kp, const SpecCtx &sc, uint64_t lo, uint64_t hi, uint32_t *row) {
+  const uint8_t *end = kp.buf + kp.len;
+  const uint32_t za = kp.big ? 8u : 11u, zb = kp.big ? 12u : 15u;  // the zero high bytes of incl / orig
+  uint64_t c = lo;
+  const uint8_t *a16 = align16(kp.buf + c);
+  SpWin W;
+  win_load(a16, end, W);
+  while (c < hi) {
+    const uint32_t r0 = (uint32_t)((uintptr_t)(kp.buf + c) & 15u);  // candidates r0 .. 95 of the window
+    const uint64_t cn = c + (96u - r0);
+    const bool more = cn < hi;
+    SpWin Wn;
+    if (more) win_load(a16 + 96, end, Wn);  // in flight while this window is screened
+    win_store(W, row);
+    uint64_t z0 = 0, z1 = 0;  // bit b: window byte b is zero (b < 112)
+#pragma unroll
+    for (int k = 0; k < kSpWin / 16; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 4 * k + e;
+        const uint64_t b4 = zmask4(W.v[k][e]);
+        if (i < 16) z0 |= b4 << (4 * i);
+        else z1 |= b4 << (4 * (i - 16));
+      }
+    auto shr = [&](uint32_t s, uint64_t &l, uint64_t &h) {
+      l = (z0 >> s) | (z1 << (64u - s));
+      h = z1 >> s;
+    };
+    uint64_t al, ah, bl, bh;
+    shr(za, al, ah);
+    shr(zb, bl, bh);
+    uint64_t ml = al & bl & ~((1ull << r0) - 1ull), mh = ah & bh & ((1ull << 32) - 1ull);
+    while (ml | mh) {
+      uint32_t p;
+      if (ml) {
+        p = (uint32_t)__builtin_ctzll(ml);
+        ml &= ml - 1;
+      } else {
+        p = 64u + (uint32_t)__builtin_ctzll(mh);
+        mh &= mh - 1;
+      }
+      const uint64_t q = c + (p - r0);
+      if (q >= hi) return kNone;
+      uint32_t h[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t v = lds_le32(row, p + 4u * (uint32_t)k);
+        h[k] = kp.big ? __builtin_bswap32(v) : v;
+      }
+      const uint64_t avail = kp.len - q;
+      if (avail >= 16 && plaus(sc, h[0], h[1], h[2], h[3]) && avail - 16 >= h[2] && chain_ok(kp, sc, q, h[0], h[2]))
+        return q;
+    }
+    if (!more) break;
+    c = cn;
+    a16 += 96;
+    W = Wn;
+  }
+  return kNone;
+}
+
+// ---- the walk -----------------------------------------------------------------------------------
+// The serial chain (src/record.rs:30-49) from `pos` while records start before hi: one 112-B
+// window per record (the next record's in flight while this one decodes); every record's status
+// and flow go to sink(record offset, ok, flow words).  Returns the exit: the first chain offset
+// >= hi, or (chain END, Q3) the offset of the first incomplete record.
+template <class Sink>
+__device__ uint64_t lane_walk(const ParseParams &kp, uint32_t *row, uint64_t pos, uint64_t hi, uint32_t &cnt, Sink &sink) {
+  if (pos >= hi) return pos;
+  const uint8_t *end = kp.buf + kp.len;
+  SpWin W;
+  win_load(align16(kp.buf + pos), end, W);
+  for (;;) {
+    const uint8_t *pp = kp.buf + pos;
+    const uint32_t rel = (uint32_t)((uintptr_t)pp & 15u);
+    win_store(W, row);
+    uint32_t incl = lds_le32(row, rel + 8u);
+    if (kp.big) incl = __builtin_bswap32(incl);
+    const uint64_t avail = kp.len - pos;
+    if (avail < 16 || avail - 16 < incl) break;  // Err(Incomplete): the chain stops here (:37-45)
+    const uint64_t next = pos + 16 + incl;
+    const bool more = next < hi;
+    SpWin Wn;
+    if (more) win_load(align16(kp.buf + next), end, Wn);
+    FlowWords f{};
+    uint32_t st;
+    if (align16(pp) + kSpWin <= end) {
+      st = decode_fast<true>(row, rel + 16u, incl, f);
+      if (st == 0xffu) {
+        const SpRowReader r{row, rel + 16u, pp + 16, avail - 16};
+        st = decode<true>(r, incl, f);
+      }
+    } else {  // the buffer's last bytes
+      const GlobalReader r{pp + 16, avail - 16};
+      st = decode<true>(r, incl, f);
+    }
+    sink(pos, st == NPR_FLOW_OK, f);
+    ++cnt;
+    pos = next;
+    if (!more) break;
+    W = Wn;
+  }
+  return pos;
+}
+
+// a flow row as k_sparse_rows writes it (IPv6: word 0 holds the address block's payload offset)
+__device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 &r0, u32x4 &r1) {
+  const bool v6 = (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+  r0 = u32x4{v6 ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3]};
+  r1 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+}
+// the lane's Ok flows into its slots (slot k of group g, lane l at ((g cap + k) 64 + l) rows):
+// one store instruction of a wave writes 64 consecutive rows
+struct AreaSink {
+  uint32_t *slot0;  // the lane's slot 0, NULL: count only
+  uint32_t cap, okn;
+  uint64_t ovf;
+  __device__ __forceinline__ void operator()(uint64_t p, bool ok, const FlowWords &f) {
+    if (!ok) return;
+    if (okn < cap) {
+      if (slot0) {
+        u32x4 r0, r1;
+        row_image(f, p, r0, r1);
+        u32x4 *d = reinterpret_cast<u32x4 *>(slot0 + (uint64_t)okn * 64u * 8u);
+        d[0] = r0;
+        d[1] = r1;
+      }
+    } else if (ovf == kNone) {
+      ovf = p;
+    }
+    ++okn;
+  }
+};
+
+// one output row (+ the IPv6 side row: its 32 address bytes re-read from the capture)
+__device__ __forceinline__ void put_row(const ParseParams &kp, uint64_t o, u32x4 s0, u32x4 s1) {
+  const bool v6 = (s1[2] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+  u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
+  d[0] = u32x4{v6 ? 0u : s0[0], s0[1], s0[2], s0[3]};
+  d[1] = s1;
+  if (v6 && kp.flows_v6) {
+    const uint64_t p = (uint64_t)(s1[2] >> 24) | ((uint64_t)s1[3] << 8);
+    const uint8_t *end = kp.buf + kp.len, *a = kp.buf + p + 16 + s0[0];
+    const uint8_t *a4 = (const uint8_t *)((uintptr_t)a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)a & 3u);
+    uint32_t x[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) x[k] = dword_at(a4 + 4 * k, end);
+    u32x4 *d6 = reinterpret_cast<u32x4 *>(kp.flows_v6 + o * 8);
+    d6[0] = u32x4{__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                  __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(x[4], x[3], sh)};
+    d6[1] = u32x4{__builtin_amdgcn_alignbyte(x[5], x[4], sh), __builtin_amdgcn_alignbyte(x[6], x[5], sh),
+                  __builtin_amdgcn_alignbyte(x[7], x[6], sh), __builtin_amdgcn_alignbyte(x[8], x[7], sh)};
+  }
+}
+// Ok flows of an overflowing lane from rank `rank` on, straight to their rows
+struct RowSink {
+  const ParseParams *kp;
+  uint64_t base;  // the lane's first Ok flow's convert_records index
+  uint32_t rank;
+  __device__ __forceinline__ void operator()(uint64_t p, bool ok, const FlowWords &f) {
+    if (!ok) return;
+    const uint64_t g = base + rank++;
+    if (g < kp->flow_cap) {
+      u32x4 r0, r1;
+      row_image(f, p, r0, r1);
+      put_row(*kp, kp->flow_cap - 1 - g, r0, r1);
+    }
+  }
+};
+
+// =============================================================================================
+// k_sparse_walk: one lane range per lane, one 64-lane group per wave
+// =============================================================================================
+__global__ __launch_bounds__(kSpBlock) void k_sparse_walk(SparseParams sp) {
+  __shared__ uint32_t rows[kSpBlock * kSpRow];
+  const ParseParams &kp = sp.kp;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t g = blockIdx.x * (kSpBlock / 64) + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *sp.ctl = 0;  // the rows kernel runs only after a new exact scan
+  if (g >= sp.ngroups) return;  // (wave-uniform)
+  const uint64_t li = (uint64_t)g * 64 + lane;
+  const bool act = li < sp.nlanes;
+  const SpecCtx sc = spec_ctx(kp, spec_ctx_load(kp));
+  uint32_t *row = rows + threadIdx.x * kSpRow;
+  const uint64_t lo = lane_lo(sp, li);
+  const uint64_t hi = act ? sp_end(sp, (int64_t)li) : lo;
+  uint64_t entry = kNone;
+  if (act) {
+    if (li == 0 && !(kp.flags & kFlagSpecStart) && !kp.prev) {
+      entry = kp.start;
+    } else {
+      if (li == 0 && kp.prev) {  // a chained launch: where the previous one left the chain (checked by the scan)
+        const uint64_t pc = kp.prev->consumed;
+        if (pc >= lo && pc < hi) entry = pc;
+      }
+      if (entry == kNone) entry = lane_speculate(kp, sc, lo, hi, row);
+    }
+  }
+  uint32_t cnt = 0;
+  AreaSink sink{kp.flows ? sp.area + (((uint64_t)g * sp.cap) * 64u + lane) * 8u : nullptr, sp.cap, 0u, kNone};
+  uint64_t exit = 0;
+  if (entry != kNone) exit = lane_walk(kp, row, entry, hi, cnt, sink);
+  SparseLane L{entry, exit, cnt, sink.okn, sink.ovf};
+  if (act) sp.lanes[li] = L;
+  // the group's aggregate: every link consistent (no END before the last lane, no lane a record
+  // spans) -> two wave sums; otherwise the serial monoid
+  const uint32_t size = sp.nlanes - (uint64_t)g * 64 < 64 ? (uint32_t)(sp.nlanes - (uint64_t)g * 64) : 64u;
+  const Seg me = lane_seg(sp, li, L);
+  const uint64_t prev_exit = shfl_up64(me.exit);
+  const bool link_bad = act && (me.entry == kNone || (lane > 0 && me.entry != prev_exit));
+  const bool end_mid = act && lane + 1 < size && me.exit < hi;
+  Seg agg;
+  if (__ballot(link_bad || end_mid) == 0ull) {
+    uint64_t c = act ? me.cnt : 0, o = act ? me.ok : 0;
+    for (int k = 32; k > 0; k >>= 1) {
+      c += __shfl_xor(c, k);
+      o += __shfl_xor(o, k);
+    }
+    agg.entry = rl64(me.entry, 0);
+    agg.exit = rl64(me.exit, (int)size - 1);
+    agg.cnt = c;
+    agg.ok = o;
+    agg.first = (int64_t)g * 64;
+    agg.last = (int64_t)g * 64 + size - 1;
+    agg.mism = -1;
+    agg.valid = 1;
+  } else {
+    const uint64_t bnone = __ballot(me.entry == kNone);
+    agg = lane_seg(sp, (uint64_t)g * 64, SparseLane{rl64(L.entry, 0), rl64(L.exit, 0), (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0),
+                                                     (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, 0), 0});
+    for (uint32_t j = 1; j < size; ++j) {
+      const SparseLane Lj{(bnone >> j) & 1ull ? kNone : rl64(L.entry, (int)j), rl64(L.exit, (int)j),
+                          (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)j),
+                          (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, (int)j), 0};
+      agg = sp_cat(sp, agg, lane_seg(sp, (uint64_t)g * 64 + j, Lj));
+    }
+  }
+  const uint64_t has = __ballot(act && entry != kNone);
+  if (lane == 0) {
+    put_seg(sp.aggs + (uint64_t)g * kSparseAggWords, agg);
+    sp.first_entry[g] = has ? rl64(entry, __builtin_ctzll(has)) : kNone;
+  }
+}
+
+// =============================================================================================
+// k_sparse_scan: one workgroup.  Rounds of: cut the groups into runs of plainly linked groups (each
+// continues its predecessor's speculated chain exactly: those compose by sums), walk the runs from
+// the anchor (one step per run: the group the incoming position lands in must start there); if
+// nothing is contradicted, write every group's incoming chain state + the summary and stop; else
+// resolve the contradicted groups (up to kResolvers at once, one thread each) and go again.  Each
+// round settles the lowest contradiction exactly (its incoming position is exact), so rounds end.
+// (A tree of composite aggregates is not exact here: a record that spans a composite's first group
+// enters it past its entry, which only the lanes can settle.)
+// =============================================================================================
+// Group w resolved from its incoming chain state x (thread-serial): lanes a record spans are marked
+// passed over (entry = exit = the incoming position: their link is then consistent whatever they
+// speculated), mis-speculated lanes walk again from the incoming position; then the group's
+// aggregate is folded again.
+__device__ void resolve_group(const SparseParams &sp, uint32_t w, Seg s, uint32_t *row, uint32_t &rewalks) {
+  const ParseParams &kp = sp.kp;
+  const uint64_t l0 = (uint64_t)w * 64;
+  const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
+  for (uint32_t j = 0; j < size; ++j) {
+    const uint64_t li = l0 + j, hi = sp_end(sp, (int64_t)li);
+    if (s.exit < sp_end(sp, s.last)) break;  // the chain ended before this lane
+    SparseLane L = sp.lanes[li];
+    if (s.exit >= hi) {  // a record spans the lane
+      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone};
+      s.last = (int64_t)li;
+      continue;
+    }
+    if (L.entry != s.exit) {  // mis-speculated: the exact walk from the incoming position
+      uint32_t cnt = 0;
+      AreaSink sink{kp.flows ? sp.area + (((uint64_t)w * sp.cap) * 64u + j) * 8u : nullptr, sp.cap, 0u, kNone};
+      const uint64_t ex = lane_walk(kp, row, s.exit, hi, cnt, sink);
+      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf};
+      sp.lanes[li] = L;
+      ++rewalks;
+    }
+    s.exit = L.exit;
+    s.cnt += L.cnt;
+    s.ok += L.ok;
+    s.last = (int64_t)li;
+  }
+  Seg a = lane_seg(sp, l0, sp.lanes[l0]);
+  for (uint32_t j = 1; j < size; ++j) a = sp_cat(sp, a, lane_seg(sp, l0 + j, sp.lanes[l0 + j]));
+  put_seg(sp.aggs + (uint64_t)w * kSparseAggWords, a);
+}
+
+__device__ __forceinline__ void fence_agent() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
+
+// a group's plain link: it continues its predecessor's chain exactly (the predecessor did not end
+// the chain, its exit lands in this group and is this group's first lane's entry, no contradiction
+// inside): runs of plainly linked groups compose by sums
+__device__ __forceinline__ bool plain_link(const SparseParams &sp, const Seg &p, const Seg &a) {
+  return a.valid && p.exit >= sp_end(sp, p.last) && p.exit < sp_end(sp, a.last) && p.exit == a.entry;
+}
+__device__ __forceinline__ int64_t group_last_lane(const SparseParams &sp, uint64_t w) {
+  const uint64_t l = (w + 1) * 64;
+  return (int64_t)(l < sp.nlanes ? l : sp.nlanes) - 1;
+}
+// exclusive block-wide scan of (c, o, n) over kScanThreads threads
+__device__ void block_scan3(uint64_t &c, uint64_t &o, uint32_t &n, uint64_t &tc, uint64_t &to, uint32_t &tn,
+                            uint64_t *sc, uint64_t *so, uint32_t *sn) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  uint64_t ic = c, io = o;
+  uint32_t in = n;
+  for (int d = 1; d < 64; d <<= 1) {  // inclusive scan inside the wave
+    const uint64_t yc = __shfl_up(ic, d, 64), yo = __shfl_up(io, d, 64);
+    const uint32_t yn = __shfl_up(in, d, 64);
+    if ((int)lane >= d) {
+      ic += yc;
+      io += yo;
+      in += yn;
+    }
+  }
+  if (lane == 63) {
+    sc[wv] = ic;
+    so[wv] = io;
+    sn[wv] = in;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint64_t ac = 0, ao = 0;
+    uint32_t an = 0;
+    for (uint32_t k = 0; k < kScanThreads / 64; ++k) {
+      const uint64_t xc = sc[k], xo = so[k];
+      const uint32_t xn = sn[k];
+      sc[k] = ac;
+      so[k] = ao;
+      sn[k] = an;
+      ac += xc;
+      ao += xo;
+      an += xn;
+    }
+    sc[kScanThreads / 64] = ac;
+    so[kScanThreads / 64] = ao;
+    sn[kScanThreads / 64] = an;
+  }
+  __syncthreads();
+  c = sc[wv] + ic - c;
+  o = so[wv] + io - o;
+  n = sn[wv] + in - n;
+  tc = sc[kScanThreads / 64];
+  to = so[kScanThreads / 64];
+  tn = sn[kScanThreads / 64];
+  __syncthreads();
+}
+
+struct RunInfo {       // a run of plainly linked groups [s, e): the chain state it is entered with and
+  uint64_t exit, cnt, ok, g;  // the group it enters at (g = e: none, the chain ended or passes over it)
+};
+
+__global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
+  __shared__ uint64_t wsc[kScanThreads / 64 + 1], wso[kScanThreads / 64 + 1];
+  __shared__ uint32_t wsn[kScanThreads / 64 + 1];
+  __shared__ Seg badx[kResolvers];
+  __shared__ uint32_t bad[kResolvers];
+  __shared__ uint32_t nbad, first_w, fail, rewalks;
+  __shared__ uint64_t entry0;
+  __shared__ Seg E0, TOT;
+  __shared__ uint32_t rows[kResolvers * kSpRow];
+  const ParseParams &kp = sp.kp;
+  const uint32_t tid = threadIdx.x, W = sp.ngroups;
+  const uint32_t q = W ? (W + kScanThreads - 1) / kScanThreads : 1u;  // groups per thread
+  const uint32_t w0 = tid * q < W ? tid * q : W, w1 = w0 + q < W ? w0 + q : W;
+  // scan scratch: exclusive sums of the groups' records / Ok flows (W + 1 each), each group's run,
+  // the runs' first groups, the runs' entry states
+  uint64_t *scnt = sp.scan, *sok = scnt + (W + 1);
+  uint32_t *run_of = reinterpret_cast<uint32_t *>(sok + (W + 1)), *runs = run_of + W;
+  RunInfo *rinfo = reinterpret_cast<RunInfo *>(sok + (W + 1) + W);
+  auto agg = [&](uint32_t w) { return get_seg(sp.aggs + (uint64_t)w * kSparseAggWords); };
+  if (tid == 0) {
+    first_w = ~0u;
+    fail = 0;
+    rewalks = 0;
+  }
+  __syncthreads();
+  if ((kp.flags & kFlagSpecStart) && !kp.prev)  // the anchor: the first lane entry found
+    for (uint32_t w = w0; w < w1; ++w)
+      if (sp.first_entry[w] != kNone) {
+        atomicMin(&first_w, w);
+        break;
+      }
+  __syncthreads();
+  if (tid == 0) {
+    Seg E{};
+    E.entry = E.exit = kp.start;
+    E.first = E.last = -1;
+    E.mism = -1;
+    E.valid = 1;
+    uint64_t e0 = kp.start;
+    if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
+      if (kp.prev_epoch != 0 && kp.prev->epoch != kp.prev_epoch) fail = 1;  // it did not complete
+      E.entry = E.exit = kp.prev->consumed;
+      E.cnt = kp.prev->n_records;
+      E.ok = kp.prev->n_flows;
+      e0 = kp.prev->entry;
+    } else if (kp.flags & kFlagSpecStart) {
+      e0 = first_w == ~0u ? kNone : sp.first_entry[first_w];
+      E.entry = E.exit = e0 == kNone ? kp.stop : e0;
+    }
+    E0 = E;
+    entry0 = e0;
+  }
+  __syncthreads();
+  if (fail) return;  // no summary: npr_dev_check reports the previous link's failure as a timeout
+  for (uint32_t round = 0;; ++round) {
+    // every round settles the lowest contradicted group for good: more rounds than groups is a bug,
+    // and the launch then ends without a summary (npr_dev_check reports it) instead of spinning
+    if (round > W + 1) return;
+    // (1) runs of plainly linked groups; exclusive sums of records / Ok flows over the groups
+    uint64_t c = 0, o = 0;
+    uint32_t ns = 0;
+    {
+      Seg p = w0 > 0 && w0 < W ? agg(w0 - 1) : Seg{};
+      for (uint32_t w = w0; w < w1; ++w) {
+        const Seg a = agg(w);
+        ns += (w == 0 || !plain_link(sp, p, a)) ? 1u : 0u;
+        c += a.cnt;
+        o += a.ok;
+        p = a;
+      }
+    }
+    uint64_t tc, to;
+    uint32_t tn;
+    block_scan3(c, o, ns, tc, to, tn, wsc, wso, wsn);
+    {
+      Seg p = w0 > 0 && w0 < W ? agg(w0 - 1) : Seg{};
+      for (uint32_t w = w0; w < w1; ++w) {
+        const Seg a = agg(w);
+        if (w == 0 || !plain_link(sp, p, a)) runs[ns++] = w;
+        run_of[w] = ns - 1;
+        scnt[w] = c;
+        sok[w] = o;
+        c += a.cnt;
+        o += a.ok;
+        p = a;
+      }
+    }
+    if (tid == 0) {
+      scnt[W] = tc;
+      sok[W] = to;
+    }
+    fence_agent();
+    __syncthreads();
+    fence_agent();
+    // (2) the runs in order from the anchor (one thread; C3 has one run): each is entered at the
+    //     group its incoming position lands in, and a contradiction there flags the group
+    if (tid == 0) {
+      uint64_t ex = E0.exit, cn = E0.cnt, ok = E0.ok;
+      int64_t last = E0.last;
+      uint32_t nb = 0;
+      for (uint32_t r = 0; r < tn; ++r) {
+        const uint32_t e = r + 1 < tn ? runs[r + 1] : W;  // this run: groups [runs[r], e)
+        RunInfo ri{ex, cn, ok, e};
+        const int64_t run_last = group_last_lane(sp, e - 1);
+        if (ex >= sp_end(sp, last) && ex < sp_end(sp, run_last)) {  // not ended, lands in this run
+          const uint64_t g = (ex - kp.start) / (64 * sp.span);
+          ri.g = g;
+          const Seg a = agg((uint32_t)g);
+          if (!(a.valid && a.entry == ex)) {  // contradicted: resolve g from this state
+            if (nb < (uint32_t)kResolvers) {
+              Seg x{};
+              x.entry = x.exit = ex;
+              x.cnt = cn;
+              x.ok = ok;
+              x.first = x.last = (int64_t)g * 64 - 1;
+              x.mism = -1;
+              x.valid = 1;
+              bad[nb] = (uint32_t)g;
+              badx[nb] = x;
+            }
+            ++nb;
+          }
+          ex = agg(e - 1).exit;  // (contradicted: as if its resolution rejoins the speculated chain)
+          cn += scnt[e] - scnt[g];
+          ok += sok[e] - sok[g];
+          last = run_last;
+        } else if (ex >= sp_end(sp, last)) {  // one record spans the whole run
+          last = run_last;
+        }
+        rinfo[r] = ri;
+      }
+      nbad = nb;
+      Seg t{};
+      t.exit = ex;
+      t.cnt = cn;
+      t.ok = ok;
+      TOT = t;
+    }
+    fence_agent();
+    __syncthreads();
+    fence_agent();
+    if (nbad == 0) {  // every link exact: each group's incoming chain state, and the summary
+      for (uint32_t w = w0; w < w1; ++w) {
+        const RunInfo ri = rinfo[run_of[w]];
+        SparsePre pr{ri.exit, ri.cnt, ri.ok, 0};
+        if (w > ri.g) {
+          pr.exit = agg(w - 1).exit;
+          pr.cnt = ri.cnt + scnt[w] - scnt[ri.g];
+          pr.ok = ri.ok + sok[w] - sok[ri.g];
+        }
+        sp.pre[w] = pr;
+      }
+      if (tid == 0) {
+        npr_summary *sm = kp.summary;
+        sm->n_records = TOT.cnt;
+        sm->n_flows = TOT.ok;
+        sm->consumed = TOT.exit;
+        sm->flags = (kp.flows && TOT.ok > kp.flow_cap) ? NPR_SUMMARY_FLOW_OVERFLOW : 0u;
+        sm->epoch = kp.epoch;
+        sm->entry = entry0;
+        __hip_atomic_store(sp.ctl, gran(kp.epoch, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kp.stats && rewalks) atomicAdd(kp.stats + kStatRewalk, rewalks);
+      }
+      return;
+    }
+    // (3) resolve the flagged groups (the lowest from its exact incoming state), then scan again
+    const uint32_t nr = nbad < (uint32_t)kResolvers ? nbad : (uint32_t)kResolvers;
+    if (tid < nr) {
+      uint32_t rw = 0;
+      resolve_group(sp, bad[tid], badx[tid], rows + tid * kSpRow, rw);
+      if (rw) atomicAdd(&rewalks, rw);
+    }
+    fence_agent();
+    __syncthreads();
+    fence_agent();
+  }
+}
+
+// =============================================================================================
+// k_sparse_rows: group w's Ok flows (file order i = 0 .. okw-1, global index O + i) to rows
+// flow_cap - 1 - (O + i); thread b writes the b-th row of the group's block, so consecutive
+// threads store consecutive rows
+// =============================================================================================
+__global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
+  __shared__ uint32_t opre[65];
+  __shared__ uint32_t okl[64];
+  __shared__ uint64_t ovf[64], hil[64];
+  __shared__ SparseLane ls[64];
+  __shared__ uint32_t rows[64 * kSpRow];
+  const ParseParams &kp = sp.kp;
+  const uint32_t w = blockIdx.x, tid = threadIdx.x;
+  if (__hip_atomic_load(sp.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gran(kp.epoch, 1)) return;
+  const SparsePre P = sp.pre[w];
+  const uint64_t l0 = (uint64_t)w * 64;
+  const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
+  if (tid < size) ls[tid] = sp.lanes[l0 + tid];
+  __syncthreads();
+  if (tid == 0) {  // which lanes the exact chain runs through (every link is consistent now)
+    uint64_t s = P.exit;
+    bool ended = s < sp_end(sp, (int64_t)l0 - 1);
+    uint32_t acc = 0;
+    for (uint32_t j = 0; j < 64; ++j) {
+      opre[j] = acc;
+      okl[j] = 0;
+      if (j >= size || ended) continue;
+      const uint64_t hi = sp_end(sp, (int64_t)(l0 + j));
+      if (s >= hi) continue;  // a record spans the lane
+      const SparseLane &L = ls[j];
+      okl[j] = L.ok;
+      ovf[j] = L.ovf;
+      hil[j] = hi;
+      acc += L.ok;
+      s = L.exit;
+      ended = s < hi;
+    }
+    opre[64] = acc;
+  }
+  __syncthreads();
+  const uint32_t okw = opre[64];
+  const uint64_t O = P.ok;
+  for (uint32_t b = tid; b < okw; b += kSpBlock) {
+    const uint32_t i = okw - 1 - b;
+    const uint64_t gi = O + i;
+    if (gi >= kp.flow_cap) continue;
+    uint32_t j = 0;  // the lane of flow i: the last j with opre[j] <= i
+#pragma unroll
+    for (uint32_t step = 32; step; step >>= 1)
+      if (opre[j + step] <= i) j += step;
+    const uint32_t r = i - opre[j];
+    if (r >= sp.cap) continue;  // past the lane's slots: its overflow walk below
+    const u32x4 *src = reinterpret_cast<const u32x4 *>(sp.area + (((uint64_t)w * sp.cap + r) * 64u + j) * 8u);
+    put_row(kp, kp.flow_cap - 1 - gi, src[0], src[1]);
+  }
+  if (tid < 64 && okl[tid] > sp.cap) {  // a lane with more Ok flows than slots: the rest walked again
+    RowSink sink{&kp, O + opre[tid], sp.cap};
+    uint32_t cnt = 0;
+    (void)lane_walk(kp, rows + tid * kSpRow, ovf[tid], hil[tid], cnt, sink);
+  }
+}
+
+}  // namespace
+
+hipError_t launch_sparse(const SparseParams &sp, hipStream_t s) {
+  if (sp.ngroups) {
+    hipLaunchKernelGGL(k_sparse_walk, dim3((sp.ngroups + kSpBlock / 64 - 1) / (kSpBlock / 64)), dim3(kSpBlock), 0, s, sp);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_sparse_scan, dim3(1), dim3(kScanThreads), 0, s, sp);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !sp.ngroups || !sp.kp.flows) return e;
+  hipLaunchKernelGGL(k_sparse_rows, dim3(sp.ngroups), dim3(kSpBlock), 0, s, sp);
+  return hipGetLastError();
+}
+
+}  // namespace npr

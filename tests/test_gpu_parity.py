@@ -92,7 +92,11 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     64-wave group, speculation at range starts deep inside the capture); light="decode" the
     two-pass kernels (NPR_OPT_RESIDENT off); light="batch" / "batch_wN" the capture inside a batched
     launch (k_parse_batch), the latter with at most N waves per capture (deferred tiles re-read
-    through a ring that holds the next capture's staged tiles)."""
+    through a ring that holds the next capture's staged tiles); light="sparse" the sparse record walk
+    forced (NPR_OPT_SPARSE 2), "sparse_sN" with lane ranges of N bytes, "..._cK" with K Ok-flow
+    slots per lane (lanes past their slots walk the rest again when rows are written)."""
+    if isinstance(light, str) and light.startswith("sparse"):
+        return check_sparse(blob, start, endianness, ws, light)
     if isinstance(light, str) and light.startswith("batch"):
         ctx = npr.context(0)
         cap = int(light[7:]) if light.startswith("batch_w") else 1
@@ -136,6 +140,42 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     return sm
 
 
+def sparse_opts(light):
+    """NPR_OPT_SPARSE / NPR_OPT_SPARSE_CAP values of a "sparse[_sN][_cK]" variant."""
+    mode, cap = 2, 0
+    for part in light.split("_")[1:]:
+        if part[0] == "s":
+            mode = int(part[1:])
+        elif part[0] == "c":
+            cap = int(part[1:])
+    return mode, cap
+
+
+class sparse_forced:
+    """Every flows-only launch of the context runs the sparse record walk inside the block."""
+    def __init__(self, light="sparse"):
+        self.mode, self.cap = sparse_opts(light)
+        self.ctx = npr.context(0)
+
+    def __enter__(self):
+        lib, h = self.ctx.lib, self.ctx.handle
+        self.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, self.mode))
+        self.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE_CAP, self.cap))
+        return self
+
+    def __exit__(self, *exc):
+        lib, h = self.ctx.lib, self.ctx.handle
+        self.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, 0))
+        self.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE_CAP, 0))
+
+
+def check_sparse(blob, start, endianness, ws, light):
+    with sparse_forced(light) as f:
+        sm = check_parity(blob, start, endianness, ws, light=True)
+        assert f.ctx.lib.npr_ctx_last_pass(f.ctx.handle) == _abi.PASS_SPARSE
+    return sm
+
+
 def first_diff(a, b):
     n = min(len(a), len(b))
     for i in range(n):
@@ -168,9 +208,13 @@ def test_kat_frames_as_records(name):
 
 # ---- synthetic corpora ---------------------------------------------------------------------
 # resident_w16 / _w48: whole 16-wave workgroups (one and three), long ranges with deferred tiles
-LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode", "batch", "batch_w7", "batch_w100"],
+# sparse: the sparse record walk forced; _s256: 256-B lane ranges (records span many lanes, most
+# lanes speculate inside payloads); _s4096_c2: two Ok-flow slots per lane (the overflow walk)
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode", "batch", "batch_w7", "batch_w100",
+                                          "sparse", "sparse_s256", "sparse_s4096_c2"],
                                 ids=["full", "resident", "resident_w7", "resident_w100", "resident_w16",
-                                     "resident_w48", "two_pass", "batch", "batch_w7", "batch_w100"])
+                                     "resident_w48", "two_pass", "batch", "batch_w7", "batch_w100",
+                                     "sparse", "sparse_s256", "sparse_s4096_c2"])
 
 
 @LIGHT
@@ -403,6 +447,42 @@ def test_chunked_packing_pass(corpus, chunk):
         check_chunked(blob, chunk)
     finally:
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
+
+
+@pytest.mark.parametrize("chunk", [40_000, 333_333])
+@pytest.mark.parametrize("corpus", ["c3", "quirk", "adversarial", "jumbo", "v6", "tails"])
+def test_chunked_sparse_links(corpus, chunk):
+    """Sparse walks as chained links (each continues the previous link's device summary): lane 0
+    starts at the previous link's exit, the scan checks it against that summary."""
+    blob = {"c3": lambda: synth.variable_mix(8_000),
+            "quirk": lambda: synth.quirk_corpus(6_000, seed=62),
+            "adversarial": lambda: synth.quirk_corpus(3_000, seed=63, fake_every=3, zero_every=7, jumbo_every=150),
+            "jumbo": lambda: synth.quirk_corpus(400, seed=64, jumbo_every=2),
+            "v6": lambda: synth.quirk_corpus(5_000, seed=65, big=True),
+            "tails": lambda: synth.corrupt_midfile(synth.fixed64(20_000), at_record=7_777)}[corpus]()
+    with sparse_forced("sparse_s512_c4") as f:
+        check_chunked(blob, chunk)
+        assert f.ctx.lib.npr_ctx_last_pass(f.ctx.handle) == _abi.PASS_SPARSE
+
+
+def test_sparse_range_speculative_start():
+    """A byte range whose start is not a record boundary (the shard form): the sparse walk
+    speculates the first record like the resident pass and reports it in summary->entry."""
+    blob = synth.variable_mix(6_000)
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    offs = recs["offset"].astype(np.int64)
+    lo = int(offs[1234]) - 5                       # inside record 1233
+    stop = int(offs[4000]) + 3
+    want = recs[(offs >= int(offs[1234])) & (offs < stop)]
+    wf, _ = _oracle.convert_records(blob, want)
+    buf = to_dev(blob)
+    cap = len(blob) // 16 + 1
+    with sparse_forced("sparse_s1024"):
+        w = device.Workspace(cap, cap, records=False, status=False)
+        w.launch_range(buf, lo, stop, endianness=hdr.endianness, speculative=True)
+        sm = w.check()
+    assert sm.entry == int(offs[1234]) and sm.n_records == len(want) and sm.n_flows == len(wf)
+    assert w.flows_np().tobytes() == wf.tobytes()
 
 
 def test_chunked_bare_records_and_tiny_inputs():

@@ -70,15 +70,24 @@ def test_c3_full_8m_bit_exact():
     hdr, recs, cons, flows, _ = oracle_flows(blob)
     n = len(recs)
     assert n == 8_000_000
-    log("C3: device")
     ws = device.Workspace(record_cap=n, flow_cap=n, records=False, offsets=False, status=False,
                           flows=True, flows_v6=True)
     buf = to_dev(blob)
-    ws.launch(buf, start=24, endianness=hdr.endianness)  # chained resident launches
-    sm = ws.check()
-    assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons)
-    got = ws.flows_np()
-    assert got.tobytes() == flows.tobytes()
+    lib, h = ws.ctx.lib, ws.ctx.handle
+    # the default choice (the sparse record walk: ~800-B records), then the chained resident launches
+    for mode, want_pass in ((0, _abi.PASS_SPARSE), (1, _abi.PASS_RESIDENT)):
+        log(f"C3: device (NPR_OPT_SPARSE {mode})")
+        ws.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, mode))
+        try:
+            ws.flows.zero_()
+            ws.launch(buf, start=24, endianness=hdr.endianness)
+            sm = ws.check()
+            assert lib.npr_ctx_last_pass(h) == want_pass
+        finally:
+            ws.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, 0))
+        assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons)
+        got = ws.flows_np()
+        assert got.tobytes() == flows.tobytes()
     log("C3: ok")
 
 
