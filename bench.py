@@ -86,21 +86,25 @@ def cpu_baseline(blob, n_records, budget_s, sample):
                       f"parallel extract_flow); {p1} passes in {e1:.1f} s on 1 core"}
 
 
+# The PMC summaries bench.py quotes as roofline.traffic: fixed names, rewritten once per round by
+# scripts/pmc.sh + scripts/pmc_summary.py (never "the newest file": an experiment's summary must not
+# become the bench's traffic by sorting first).
+PMC_SUMMARY = {"c2": "r04_pmc_c2.json", "c3": "r04_pmc_c3.json"}
+
+
 def pmc_traffic(records, config="c2"):
-    """HBM-side bytes per launch (C2) or per capture (C3: all its chained links) from the newest
-    committed PMC summary of this workload (profiles/), or None.  Collected by scripts/pmc.sh:
-    FETCH_SIZE x2 + WRITE_SIZE."""
-    import glob
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "r*_pmc_summary.json")), reverse=True):
-        try:
-            d = json.load(open(f))
-        except (OSError, ValueError):
-            continue
-        if config == "c2" and records == 1_000_000 and d.get("workload", "").startswith("C2"):
-            return d.get("traffic_bytes_per_launch"), os.path.basename(f)
-        if config == "c3" and records == 8_000_000 and d.get("workload", "").startswith("C3"):
-            return d.get("traffic_bytes_per_capture"), os.path.basename(f)  # all chained links of one capture
-    return None, None
+    """HBM-side bytes per launch (C2) or per capture (C3: every kernel of one step) from this round's
+    committed PMC summary of the workload (profiles/PMC_SUMMARY[config]), or None: FETCH_SIZE x2 +
+    WRITE_SIZE (the gfx950 correction of MI355X_MICROARCH.md)."""
+    name = PMC_SUMMARY.get(config)
+    want = {"c2": 1_000_000, "c3": 8_000_000}.get(config)
+    if not name or records != want:
+        return None, None
+    try:
+        d = json.load(open(os.path.join(REPO, "profiles", name)))
+    except (OSError, ValueError):
+        return None, None
+    return d.get("traffic_bytes_per_step"), name
 
 
 def roofline(read_b, write_b, kern_ms, traffic=None, traffic_src=None, stream_b=None):
@@ -133,9 +137,12 @@ def run_single(args, dev, local):
                           flows=True, flows_v6=True)
     stream = torch.cuda.Stream(dev)  # an explicit stream: events bracket exactly our launches
     torch.cuda.set_stream(stream)
+    if args.sparse_span:
+        ws.ctx.check(ws.ctx.lib.npr_ctx_set_option(ws.ctx.handle, npr._abi.OPT_SPARSE, args.sparse_span))
 
     # correctness gate for the measured configuration (tests/test_gpu_scale.py compares it bit for bit)
     ws.launch(bufs[0], start=24, endianness=hdr.endianness)
+    pass_ran = {1: "two-pass", 2: "resident", 4: "batched", 8: "sparse"}.get(ws.ctx.lib.npr_ctx_last_pass(ws.ctx.handle), "?")
     if args.no_gate:  # timing-only ablation builds (make ablate): their results are not checked
         torch.cuda.synchronize()
         n_flows = n
@@ -164,18 +171,23 @@ def run_single(args, dev, local):
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     if args.stats:
         stats_dump(ws, bufs, hdr, copies, 0)
-    read_b = len(blob)   # every byte of the capture is read (C2: = SURVEY 8d's 16 + min(incl, 64) per record)
+    # algorithmic bytes: 16 + min(incl, 64) read per record, 32 written per Ok flow.
+    # C2 (80-B records): every byte of the capture.  C3 (frames >= 64 B): 80 B of each ~800-B record.
+    read_b = len(blob) if args.config != "c3" else 80 * n
     write_b = 32 * n_flows
     traffic, src = pmc_traffic(n, args.config) if args.config in ("c2", "c3") else (None, None)
     out = base_line(args, 1, wall, n, len(blob))
-    out["config"].update({"records_per_gpu": n, "capture_bytes": len(blob), "parallelism": "single GPU"})
+    out["config"].update({"records_per_gpu": n, "capture_bytes": len(blob), "parallelism": "single GPU",
+                          "pass": pass_ran})
     out["roofline"] = roofline(read_b, write_b, kern_ms, traffic, src, stream_b=len(blob) - 24)
     if c3:
-        sd = 16 * n + 64 * n  # SURVEY 8d bytes of C3: 16 + min(incl, 64) read per record (+ 32 written)
-        out["roofline"]["survey_8d_bytes_per_launch"] = sd + write_b
-        out["roofline"]["survey_8d_frac"] = round((sd + write_b) / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
-        out["roofline"]["note"] = ("C3 records are ~800 B: record boundaries are unknown until the chain is walked, "
-                                   "so the whole capture streams (achieved/frac use the stream bytes)")
+        out["roofline"]["survey_8d_bytes_per_launch"] = read_b + write_b
+        out["roofline"]["survey_8d_frac"] = out["roofline"]["frac"]
+        out["roofline"]["note"] = ("C3: one step = the sparse record walk (k_sparse_walk: header hops, one 80-B window "
+                                   "per record), k_sparse_scan and k_sparse_rows; achieved = SURVEY 8d bytes / step time "
+                                   "(HIP events over the stream); stream_GBps = the capture's bytes / step time"
+                                   if pass_ran == "sparse" else
+                                   "C3 through the resident pass (every byte streams); achieved uses SURVEY 8d bytes")
     if args.config == "c2" and args.batch > 1:
         out["batched"] = batched_line(args, bufs, hdr, n, local, stream, read_b, write_b)
     if not args.no_cpu:
@@ -384,6 +396,8 @@ def parse_args(argv=None):
     ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
     ap.add_argument("--batch", type=int, default=8,
                     help="c2: also time K captures per launch (npr_dev_parse_extract_batch; the `batched` field; 1 = off)")
+    ap.add_argument("--sparse-span", type=int, default=0,
+                    help="c3: force the sparse record walk with lane ranges of N bytes (NPR_OPT_SPARSE N >= 64; 0 = auto)")
     ap.add_argument("--sharded", action="store_true",
                     help="c4 through the multi-GPU step (RCCL exchange + gather) even at N=1")
     # the launcher alone, on CPU: every rank joins a gloo group and rank 0 prints the world it saw

@@ -172,7 +172,7 @@ constexpr uint64_t kProbeBytes = 256u << 10;        // walked from the known fir
 constexpr uint64_t kSparseMinBytes = 16ull << 20;   // auto: the sparse walk for ranges from this size on
 constexpr uint64_t kSparseMinMean = 384;            // ... of at least this many bytes per record (16 + incl)
 constexpr uint64_t kSparseSpanDefault = 16u << 10;  // lane range when the density is unknown
-constexpr uint64_t kSparseSpanRecords = 24;         // lane range = this many mean records
+constexpr uint64_t kSparseSpanRecords = 40;         // lane range = this many mean records (slots: 64)
 // Records from the exact record start `start` in the capture's first kProbeBytes: *n and their
 // bytes per record (header included), 0 when fewer than 16 fit.  One pinned D2H copy and a sync,
 // remembered per capture (the choice of pass never changes a result: a stale entry costs time only).
@@ -415,7 +415,7 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
       c->sparse_mode = value;
       return NPR_OK;
     case NPR_OPT_SPARSE_CAP:  // Ok-flow slots per lane (0 = the default)
-      if (value < 0 || value > 4096) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE_CAP: 0 .. 4096");
+      if (value < 0 || value > 64) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE_CAP: 0 .. 64");
       c->sparse_cap = (uint32_t)value;
       return NPR_OK;
     case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first
@@ -690,7 +690,8 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
   sp.cap = c->sparse_cap ? c->sparse_cap : npr::kSparseCapDefault;
   auto a256 = [](uint64_t x) { return (x + 255) & ~255ull; };
   const uint64_t o_agg = a256(sp.nlanes * sizeof(npr::SparseLane)), o_first = o_agg + a256(ng * npr::kSparseAggWords * 8),
-                 o_pre = o_first + a256(ng * 8), o_scan = o_pre + a256(ng * sizeof(npr::SparsePre)),
+                 o_lite = o_first + a256(ng * 8), o_pre = o_lite + a256(3 * ng * 8),
+                 o_scan = o_pre + a256(ng * sizeof(npr::SparsePre)),
                  o_ctl = o_scan + a256(npr::sparse_scan_words(ng) * 8), o_area = o_ctl + 256,
                  total = o_area + (o->flows ? ng * sp.cap * 64 * 32 : 0);
   npr_status st = ensure(c, c->sparse, total);
@@ -701,6 +702,7 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
   sp.first_entry = (uint64_t *)(b + o_first);
   sp.pre = (npr::SparsePre *)(b + o_pre);
   sp.scan = (uint64_t *)(b + o_scan);
+  sp.lite = (uint64_t *)(b + o_lite);
   sp.ctl = (uint64_t *)(b + o_ctl);
   sp.area = o->flows ? (uint32_t *)(b + o_area) : nullptr;
   if ((st = next_epoch(c, s))) return st;

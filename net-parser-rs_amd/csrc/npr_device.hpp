@@ -82,6 +82,8 @@ struct GlobalReader {
 // bit-identical to decode<> for these shapes.  Returns 0xff for any other frame (the caller then
 // runs the general decode<>).
 // ---------------------------------------------------------------------------------------------
+template <bool FIELDS, bool BALLOT4>
+__device__ __forceinline__ uint32_t decode_fast_core(uint32_t (&a)[17], uint32_t n, FlowWords &f, bool valid);
 // A16: w is 16-byte aligned in LDS (the staged tiles; not the per-record rows)
 // valid: lanes whose result is used (A16: when every such lane is IPv4, the IPv4-only variant)
 template <bool FIELDS, bool A16 = false>
@@ -136,6 +138,13 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
       prev = nx;
     }
   }
+  return decode_fast_core<FIELDS, A16>(a, n, f, valid);
+}
+
+// decode_fast on the frame's first 68 bytes, a[k] = payload bytes [4k, 4k + 4) (any source).
+// BALLOT4: when every valid lane is IPv4, the IPv4-only variant (a[12..16] are then not read).
+template <bool FIELDS, bool BALLOT4>
+__device__ __forceinline__ uint32_t decode_fast_core(uint32_t (&a)[17], uint32_t n, FlowWords &f, bool valid) {
   // pin the window in registers: otherwise the backend turns the IPv4/IPv6 selects below into
   // divergent branches that each load only their own words (select-to-branch on loads)
 #pragma unroll
@@ -193,7 +202,7 @@ __device__ __forceinline__ uint32_t decode_fast(const uint32_t *w, uint32_t rel,
   }
   return (v4 | v6) ? (st3 ? st3 : st4) : 0xffu;
   };
-  if (A16 && __ballot(valid & !is4) == 0ull) return core(std::true_type{});
+  if (BALLOT4 && __ballot(valid & !is4) == 0ull) return core(std::true_type{});
   return core(std::false_type{});
 }
 

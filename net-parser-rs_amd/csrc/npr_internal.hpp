@@ -177,7 +177,8 @@ struct SparseLane {  // one lane range's walk (k_sparse_walk; rewritten exact by
   uint64_t entry;    // first record (speculated, or exact), ~0 = none found
   uint64_t exit;     // chain position after the range, or the incomplete record (chain END)
   uint32_t cnt, ok;  // records / Ok flows
-  uint64_t ovf;      // the first record whose Ok flow has no slot (~0: every Ok flow has one)
+  uint64_t ovf;      // the first record without a slot (record `cap`; ~0: every record has one)
+  uint64_t okmask;   // bit k: record k (slot k) is an Ok flow
 };
 struct SparsePre {   // exact chain state before a 64-lane group (k_sparse_scan -> k_sparse_rows)
   uint64_t exit, cnt, ok, pad;
@@ -195,11 +196,14 @@ struct SparseParams {
   uint64_t *first_entry;  // [ngroups]: the group's first lane entry found (speculative starts)
   SparsePre *pre;         // [ngroups]
   uint64_t *ctl;          // [0] = {epoch, 1} once the scan finished exact (the row kernel checks it)
-  uint32_t *area;         // [ngroups][cap][64] rows of 8 words (Ok flows in row image, IPv6: word 0 = v6 offset)
+  uint32_t *area;         // slots: 32-B row (group cap + k) 64 + lane = record k of the lane
+                          // (row image; IPv6: word 0 = the address block's payload offset)
   uint64_t *scan;         // k_sparse_scan's scratch: sparse_scan_words(ngroups) words
+  uint64_t *lite;         // the aggregates' link fields as arrays: entry [ngroups], exit [ngroups],
+                          // cnt | ok << 32 | valid << 63 [ngroups] (the scan's fast path loads these)
 };
 constexpr uint64_t sparse_scan_words(uint64_t ngroups) { return 7 * ngroups + 2; }
 hipError_t launch_sparse(const SparseParams &sp, hipStream_t s);
-constexpr uint32_t kSparseCapDefault = 64;
+constexpr uint32_t kSparseCapDefault = 64;  // slots per lane (<= 64: one mask word)
 
 }  // namespace npr

@@ -32,17 +32,20 @@
 namespace npr {
 namespace {
 
+#ifndef NPR_SP_WAVES
+#define NPR_SP_WAVES 4
+#endif
 constexpr int kSpBlock = 256;                // walk / rows kernels: four 64-lane groups per workgroup
-constexpr int kSpWin = 112;                  // bytes loaded per record: [header & ~15, +112)
+constexpr int kSpWin = 112;                  // a record's full window: [header & ~15, +112) (80 B in the fast path)
 constexpr int kSpRow = kSpWin / 4 + 1;       // a lane's LDS row (odd dword stride: conflict-free)
-constexpr int kScanThreads = 1024;           // k_sparse_scan: one workgroup
+constexpr int kScanThreads = 256;            // k_sparse_scan: one workgroup (at 1024 threads its serial
+                                             // paths spilled to scratch: 37 us for the fast path alone)
 constexpr int kResolvers = 256;              // groups resolved per scan round
-static_assert(15 + 16 + 18 * 4 <= kSpWin, "header + decode_fast's 18-word window fit the row at any misalignment");
+constexpr uint32_t kScanWin = 2048;          // groups staged in LDS at a time by the scan's fast path
+static_assert(15 + 16 + 17 * 4 + 4 <= kSpWin, "header + decode_fast's 68-B window fit the row at any misalignment");
 
 typedef const __attribute__((address_space(1))) u32x4 *gv4_t;  // global (not flat) loads: vmcnt only
-struct SpWin {
-  u32x4 v[kSpWin / 16];
-};
+constexpr int kSpWords = kSpWin / 4;  // a record's window in registers: words [4 k, 4 k + 4) = chunk k
 
 __device__ __forceinline__ const uint8_t *align16(const uint8_t *p) {
   return (const uint8_t *)((uintptr_t)p & ~(uintptr_t)15);
@@ -57,25 +60,48 @@ __device__ __noinline__ uint32_t tail_dword(const uint8_t *p, const uint8_t *end
 __device__ __forceinline__ uint32_t dword_at(const uint8_t *p, const uint8_t *end) {
   return p + 4 <= end ? *reinterpret_cast<const uint32_t *>(p) : (p < end ? tail_dword(p, end) : 0u);
 }
-// the window [a16, a16 + 112) into registers (seven dwordx4 issued back to back); the last bytes
-// of the buffer dword by dword
-__device__ __forceinline__ void win_load(const uint8_t *a16, const uint8_t *end, SpWin &W) {
-  if (a16 + kSpWin <= end) {
+// chunks [K0, K1) of the window at a16 (16 B each) into w[4 K0 .. 4 K1): dwordx4 loads issued back
+// to back, or dword by dword for the buffer's last bytes
+template <int K0, int K1>
+__device__ __forceinline__ void load_chunks(const uint8_t *a16, const uint8_t *end, uint32_t (&w)[kSpWords]) {
+  if (a16 + 16 * K1 <= end) {
     const gv4_t s = (gv4_t)(uintptr_t)a16;
 #pragma unroll
-    for (int k = 0; k < kSpWin / 16; ++k) W.v[k] = s[k];
+    for (int k = K0; k < K1; ++k) {
+      const u32x4 v = s[k];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[4 * k + e] = v[e];
+    }
   } else {
 #pragma unroll
-    for (int k = 0; k < kSpWin / 16; ++k)
+    for (int k = K0; k < K1; ++k)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) W.v[k][e] = dword_at(a16 + 16 * k + 4 * e, end);
+      for (int e = 0; e < 4; ++e) w[4 * k + e] = dword_at(a16 + 16 * k + 4 * e, end);
   }
 }
-__device__ __forceinline__ void win_store(const SpWin &W, uint32_t *row) {
+// lanes whose bit of m is set: a, the others: b
+__device__ __forceinline__ uint32_t vsel(uint64_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
+}
+// Window words at a per-lane byte offset, with no register indexing: word (off >> 2) + j is chosen
+// by two selects (off & 8, off & 4) and shifted by off & 3 (v_alignbyte).
+// a[k] = window bytes [base + off + 4k, +4) for k < K (base a multiple of 4, off < 16)
+template <int BASE, int K, int N>
+__device__ __forceinline__ void words_at(const uint32_t (&w)[kSpWords], uint32_t off, uint32_t (&a)[N]) {
+  static_assert(BASE / 4 + K + 4 <= kSpWords, "window words");
+  // (v_cndmask by hand: a C select between two elements of one array is folded into an indexed
+  // access, which puts the array in scratch memory)
+  const uint64_t b1 = __ballot((off & 8u) != 0), b0 = __ballot((off & 4u) != 0);
+  const uint32_t sh = off & 3u;
+  uint32_t S[K + 2], T[K + 1];
 #pragma unroll
-  for (int k = 0; k < kSpWin / 16; ++k)
+  for (int m = 0; m < K + 2; ++m) S[m] = vsel(b1, w[BASE / 4 + 2 + m], w[BASE / 4 + m]);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) row[4 * k + e] = W.v[k][e];
+  for (int m = 0; m < K + 1; ++m) T[m] = vsel(b0, S[m + 1], S[m]);
+#pragma unroll
+  for (int k = 0; k < K; ++k) a[k] = __builtin_amdgcn_alignbyte(T[k + 1], T[k], sh);
 }
 
 // payload reader over a lane's staged window, global bytes (bounds-checked) past it
@@ -146,6 +172,12 @@ __device__ __forceinline__ void put_seg(uint64_t *d, const Seg &s) {
   d[6] = (uint64_t)s.mism;
   d[7] = s.valid;
 }
+// a group aggregate's link fields into the scan's arrays (group g of ng)
+__device__ __forceinline__ void put_lite(const SparseParams &sp, uint32_t g, const Seg &s) {
+  sp.lite[g] = s.entry;
+  sp.lite[sp.ngroups + g] = s.exit;
+  sp.lite[2 * (uint64_t)sp.ngroups + g] = (s.cnt & 0xffffffffull) | ((s.ok & 0x7fffffffull) << 32) | ((uint64_t)(s.valid != 0) << 63);
+}
 __device__ __forceinline__ Seg get_seg(const uint64_t *d) {
   Seg s;
   s.entry = d[0];
@@ -196,111 +228,134 @@ __device__ bool chain_ok(const ParseParams &kp, const SpecCtx &sc, uint64_t q0, 
   }
   return true;
 }
-// The first plausible record start in [lo, hi), kNone if none.  Windows of 96 candidate offsets:
-// every candidate needs the high bytes of incl_len and orig_len zero (both <= 2^18), which one
-// zero-byte mask over the window screens at once; the survivors are checked on their own header
-// (plaus(), the payload fits) and their chain (chain_ok()), in offset order.
-__device__ uint64_t lane_speculate(const ParseParams &kp, const SpecCtx &sc, uint64_t lo, uint64_t hi, uint32_t *row) {
+// The first plausible record start in [lo, hi), kNone if none.  Windows of 64 candidate offsets
+// (80 B loaded): every candidate needs the high bytes of incl_len and orig_len zero (both <= 2^18),
+// which one zero-byte mask over the window screens at once; the survivors are checked on their
+// own header (plaus(), the payload fits) and their chain (chain_ok()), in offset order.
+__device__ __forceinline__ uint64_t lane_speculate(const ParseParams &kp, const SpecCtx &sc, uint64_t lo, uint64_t hi,
+                                                   uint32_t *row) {
   const uint8_t *end = kp.buf + kp.len;
   const uint32_t za = kp.big ? 8u : 11u, zb = kp.big ? 12u : 15u;  // the zero high bytes of incl / orig
   uint64_t c = lo;
   const uint8_t *a16 = align16(kp.buf + c);
-  SpWin W;
-  win_load(a16, end, W);
+  uint32_t w[kSpWords], wn[kSpWords];
+  load_chunks<0, 5>(a16, end, w);
   while (c < hi) {
-    const uint32_t r0 = (uint32_t)((uintptr_t)(kp.buf + c) & 15u);  // candidates r0 .. 95 of the window
-    const uint64_t cn = c + (96u - r0);
+    const uint32_t r0 = (uint32_t)((uintptr_t)(kp.buf + c) & 15u);  // candidates r0 .. 63 of the window
+    const uint64_t cn = c + (64u - r0);
     const bool more = cn < hi;
-    SpWin Wn;
-    if (more) win_load(a16 + 96, end, Wn);  // in flight while this window is screened
-    win_store(W, row);
-    uint64_t z0 = 0, z1 = 0;  // bit b: window byte b is zero (b < 112)
+    if (more) load_chunks<0, 5>(a16 + 64, end, wn);  // in flight while this window is screened
+    uint64_t z0 = 0, z1 = 0;  // bit b: window byte b is zero (b < 80)
 #pragma unroll
-    for (int k = 0; k < kSpWin / 16; ++k)
+    for (int i = 0; i < 16; ++i) z0 |= (uint64_t)zmask4(w[i]) << (4 * i);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int i = 4 * k + e;
-        const uint64_t b4 = zmask4(W.v[k][e]);
-        if (i < 16) z0 |= b4 << (4 * i);
-        else z1 |= b4 << (4 * (i - 16));
-      }
-    auto shr = [&](uint32_t s, uint64_t &l, uint64_t &h) {
-      l = (z0 >> s) | (z1 << (64u - s));
-      h = z1 >> s;
-    };
-    uint64_t al, ah, bl, bh;
-    shr(za, al, ah);
-    shr(zb, bl, bh);
-    uint64_t ml = al & bl & ~((1ull << r0) - 1ull), mh = ah & bh & ((1ull << 32) - 1ull);
-    while (ml | mh) {
-      uint32_t p;
-      if (ml) {
-        p = (uint32_t)__builtin_ctzll(ml);
-        ml &= ml - 1;
-      } else {
-        p = 64u + (uint32_t)__builtin_ctzll(mh);
-        mh &= mh - 1;
-      }
-      const uint64_t q = c + (p - r0);
-      if (q >= hi) return kNone;
-      uint32_t h[4];
+    for (int i = 0; i < 4; ++i) z1 |= (uint64_t)zmask4(w[16 + i]) << (4 * i);
+    uint64_t m = ((z0 >> za) | (z1 << (64u - za))) & ((z0 >> zb) | (z1 << (64u - zb))) & ~((1ull << r0) - 1ull);
+    if (__ballot(m != 0ull)) {
+      if (m) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t v = lds_le32(row, p + 4u * (uint32_t)k);
-        h[k] = kp.big ? __builtin_bswap32(v) : v;
+        for (int j = 0; j < 20; ++j) row[j] = w[j];
       }
-      const uint64_t avail = kp.len - q;
-      if (avail >= 16 && plaus(sc, h[0], h[1], h[2], h[3]) && avail - 16 >= h[2] && chain_ok(kp, sc, q, h[0], h[2]))
-        return q;
+      while (m) {
+        const uint32_t p = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t q = c + (p - r0);
+        if (q >= hi) return kNone;
+        uint32_t h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t v = lds_le32(row, p + 4u * (uint32_t)k);
+          h[k] = kp.big ? __builtin_bswap32(v) : v;
+        }
+        const uint64_t avail = kp.len - q;
+        if (avail >= 16 && plaus(sc, h[0], h[1], h[2], h[3]) && avail - 16 >= h[2] && chain_ok(kp, sc, q, h[0], h[2]))
+          return q;
+      }
     }
     if (!more) break;
     c = cn;
-    a16 += 96;
-    W = Wn;
+    a16 += 64;
+#pragma unroll
+    for (int j = 0; j < 20; ++j) w[j] = wn[j];
   }
   return kNone;
 }
 
 // ---- the walk -----------------------------------------------------------------------------------
-// The serial chain (src/record.rs:30-49) from `pos` while records start before hi: one 112-B
+// One record's status + flow from its window (w[0..19] = 80 B from the header's 16-B aligned
+// start: the header and payload bytes [0, 48) at any alignment).  The IPv4 shapes decode from
+// registers; IPv6 frames take two more chunks (payload bytes up to 68); any other shape stages
+// the window in the lane's LDS row and runs the general decode<> (bytes past it from global).
+__device__ __forceinline__ uint32_t rec_decode(const ParseParams &kp, uint32_t *row, const uint8_t *pp, uint64_t avail,
+                                               uint32_t rel, uint32_t incl, uint32_t (&w)[kSpWords], FlowWords &f) {
+  const uint8_t *end = kp.buf + kp.len, *a16 = align16(pp);
+  uint32_t a[17];
+  words_at<16, 12>(w, rel, a);
+#pragma unroll
+  for (int k = 12; k < 17; ++k) a[k] = 0u;
+  const uint32_t etype = ((a[3] & 0xffu) << 8) | ((a[3] >> 8) & 0xffu);
+  const bool six = etype == 0x86ddu;
+  bool full = false;
+  if (__ballot(six)) {
+    if (six) {
+      load_chunks<5, 7>(a16, end, w);
+      words_at<16, 17>(w, rel, a);
+      full = true;
+    }
+  }
+  uint32_t st = decode_fast_core<true, true>(a, incl, f, true);
+  if (__ballot(st == 0xffu)) {
+    if (st == 0xffu) {
+      if (!full) load_chunks<5, 7>(a16, end, w);
+#pragma unroll
+      for (int j = 0; j < kSpWords; ++j) row[j] = w[j];
+      const SpRowReader r{row, rel + 16u, pp + 16, avail - 16};
+      st = decode<true>(r, incl, f);
+    }
+  }
+  return st;
+}
+
+// The serial chain (src/record.rs:30-49) from `pos` while records start before hi: one 80-B
 // window per record (the next record's in flight while this one decodes); every record's status
 // and flow go to sink(record offset, ok, flow words).  Returns the exit: the first chain offset
 // >= hi, or (chain END, Q3) the offset of the first incomplete record.
 template <class Sink>
-__device__ uint64_t lane_walk(const ParseParams &kp, uint32_t *row, uint64_t pos, uint64_t hi, uint32_t &cnt, Sink &sink) {
+__device__ __forceinline__ uint64_t lane_walk(const ParseParams &kp, uint32_t *row, uint64_t pos, uint64_t hi,
+                                              uint32_t &cnt, Sink &sink) {
   if (pos >= hi) return pos;
   const uint8_t *end = kp.buf + kp.len;
-  SpWin W;
-  win_load(align16(kp.buf + pos), end, W);
+  uint32_t w[kSpWords];
+  load_chunks<0, 5>(align16(kp.buf + pos), end, w);
   for (;;) {
     const uint8_t *pp = kp.buf + pos;
     const uint32_t rel = (uint32_t)((uintptr_t)pp & 15u);
-    win_store(W, row);
-    uint32_t incl = lds_le32(row, rel + 8u);
-    if (kp.big) incl = __builtin_bswap32(incl);
+    uint32_t h[1];
+    words_at<8, 1>(w, rel, h);  // incl_len
+    const uint32_t incl = kp.big ? __builtin_bswap32(h[0]) : h[0];
     const uint64_t avail = kp.len - pos;
     if (avail < 16 || avail - 16 < incl) break;  // Err(Incomplete): the chain stops here (:37-45)
     const uint64_t next = pos + 16 + incl;
     const bool more = next < hi;
-    SpWin Wn;
-    if (more) win_load(align16(kp.buf + next), end, Wn);
+    uint32_t wn[kSpWords];
+    if (more) load_chunks<0, 5>(align16(kp.buf + next), end, wn);
     FlowWords f{};
-    uint32_t st;
-    if (align16(pp) + kSpWin <= end) {
-      st = decode_fast<true>(row, rel + 16u, incl, f);
-      if (st == 0xffu) {
-        const SpRowReader r{row, rel + 16u, pp + 16, avail - 16};
-        st = decode<true>(r, incl, f);
-      }
-    } else {  // the buffer's last bytes
-      const GlobalReader r{pp + 16, avail - 16};
-      st = decode<true>(r, incl, f);
-    }
+#if defined(NPR_SP_EXP_HOP)  // timing experiment only: the hops, no decode, no slots
+    const uint32_t st = w[4] == 0x12345678u ? 1u : 0u;
+    asm volatile("" ::"v"(w[5]), "v"(w[19]));
+#else
+    const uint32_t st = rec_decode(kp, row, pp, avail, rel, incl, w, f);
+#endif
+#if !defined(NPR_SP_EXP_HOP) && !defined(NPR_SP_EXP_NOSLOT)
     sink(pos, st == NPR_FLOW_OK, f);
+#else
+    asm volatile("" ::"v"(st), "v"(f.d[2]));
+#endif
     ++cnt;
     pos = next;
     if (!more) break;
-    W = Wn;
+#pragma unroll
+    for (int j = 0; j < 20; ++j) w[j] = wn[j];
   }
   return pos;
 }
@@ -311,28 +366,46 @@ __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 
   r0 = u32x4{v6 ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3]};
   r1 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
 }
-// the lane's Ok flows into its slots (slot k of group g, lane l at ((g cap + k) 64 + l) rows):
-// one store instruction of a wave writes 64 consecutive rows
+// every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
+// wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded
+#ifndef NPR_SP_SLOT_POLICY
+#define NPR_SP_SLOT_POLICY 0
+#endif
+__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) {
+#if NPR_SP_SLOT_POLICY == 1
+  __builtin_nontemporal_store(v, d);
+#elif NPR_SP_SLOT_POLICY == 2
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+#elif NPR_SP_SLOT_POLICY == 3
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d), "v"(v) : "memory");
+#else
+  *d = v;
+#endif
+}
 struct AreaSink {
-  uint32_t *slot0;  // the lane's slot 0, NULL: count only
-  uint32_t cap, okn;
-  uint64_t ovf;
+  u32x4 *slot0;  // the lane's slot 0 (its first 16 B); NULL: count only
+  uint32_t cap, n, okn;
+  uint64_t okmask, ovf;
   __device__ __forceinline__ void operator()(uint64_t p, bool ok, const FlowWords &f) {
-    if (!ok) return;
-    if (okn < cap) {
+    if (n < cap) {
       if (slot0) {
         u32x4 r0, r1;
         row_image(f, p, r0, r1);
-        u32x4 *d = reinterpret_cast<u32x4 *>(slot0 + (uint64_t)okn * 64u * 8u);
-        d[0] = r0;
-        d[1] = r1;
+        slot_store(slot0 + (uint64_t)n * 128u, r0);
+        slot_store(slot0 + (uint64_t)n * 128u + 1u, r1);
       }
-    } else if (ovf == kNone) {
+      okmask |= (uint64_t)ok << n;
+    } else if (n == cap) {
       ovf = p;
     }
-    ++okn;
+    ++n;
+    okn += ok ? 1u : 0u;
   }
 };
+// slot k of lane l in group g: 32-B row ((g cap + k) 64 + l) of the area
+__device__ __forceinline__ u32x4 *slot_base(const SparseParams &sp, uint64_t g, uint32_t lane) {
+  return sp.kp.flows ? reinterpret_cast<u32x4 *>(sp.area) + ((uint64_t)g * sp.cap * 64u + lane) * 2u : nullptr;
+}
 
 // one output row (+ the IPv6 side row: its 32 address bytes re-read from the capture)
 __device__ __forceinline__ void put_row(const ParseParams &kp, uint64_t o, u32x4 s0, u32x4 s1) {
@@ -374,7 +447,7 @@ struct RowSink {
 // =============================================================================================
 // k_sparse_walk: one lane range per lane, one 64-lane group per wave
 // =============================================================================================
-__global__ __launch_bounds__(kSpBlock) void k_sparse_walk(SparseParams sp) {
+__global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(NPR_SP_WAVES))) void k_sparse_walk(SparseParams sp) {
   __shared__ uint32_t rows[kSpBlock * kSpRow];
   const ParseParams &kp = sp.kp;
   const uint32_t lane = threadIdx.x & 63u;
@@ -400,10 +473,10 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_walk(SparseParams sp) {
     }
   }
   uint32_t cnt = 0;
-  AreaSink sink{kp.flows ? sp.area + (((uint64_t)g * sp.cap) * 64u + lane) * 8u : nullptr, sp.cap, 0u, kNone};
+  AreaSink sink{slot_base(sp, g, lane), sp.cap, 0u, 0u, 0ull, kNone};
   uint64_t exit = 0;
   if (entry != kNone) exit = lane_walk(kp, row, entry, hi, cnt, sink);
-  SparseLane L{entry, exit, cnt, sink.okn, sink.ovf};
+  SparseLane L{entry, exit, cnt, sink.okn, sink.ovf, sink.okmask};
   if (act) sp.lanes[li] = L;
   // the group's aggregate: every link consistent (no END before the last lane, no lane a record
   // spans) -> two wave sums; otherwise the serial monoid
@@ -430,17 +503,18 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_walk(SparseParams sp) {
   } else {
     const uint64_t bnone = __ballot(me.entry == kNone);
     agg = lane_seg(sp, (uint64_t)g * 64, SparseLane{rl64(L.entry, 0), rl64(L.exit, 0), (uint32_t)__builtin_amdgcn_readlane((int)cnt, 0),
-                                                     (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, 0), 0});
+                                                     (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, 0), 0, 0});
     for (uint32_t j = 1; j < size; ++j) {
       const SparseLane Lj{(bnone >> j) & 1ull ? kNone : rl64(L.entry, (int)j), rl64(L.exit, (int)j),
                           (uint32_t)__builtin_amdgcn_readlane((int)cnt, (int)j),
-                          (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, (int)j), 0};
+                          (uint32_t)__builtin_amdgcn_readlane((int)sink.okn, (int)j), 0, 0};
       agg = sp_cat(sp, agg, lane_seg(sp, (uint64_t)g * 64 + j, Lj));
     }
   }
   const uint64_t has = __ballot(act && entry != kNone);
   if (lane == 0) {
     put_seg(sp.aggs + (uint64_t)g * kSparseAggWords, agg);
+    put_lite(sp, g, agg);
     sp.first_entry[g] = has ? rl64(entry, __builtin_ctzll(has)) : kNone;
   }
 }
@@ -468,15 +542,15 @@ __device__ void resolve_group(const SparseParams &sp, uint32_t w, Seg s, uint32_
     if (s.exit < sp_end(sp, s.last)) break;  // the chain ended before this lane
     SparseLane L = sp.lanes[li];
     if (s.exit >= hi) {  // a record spans the lane
-      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone};
+      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone, 0ull};
       s.last = (int64_t)li;
       continue;
     }
     if (L.entry != s.exit) {  // mis-speculated: the exact walk from the incoming position
       uint32_t cnt = 0;
-      AreaSink sink{kp.flows ? sp.area + (((uint64_t)w * sp.cap) * 64u + j) * 8u : nullptr, sp.cap, 0u, kNone};
+      AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, kNone};
       const uint64_t ex = lane_walk(kp, row, s.exit, hi, cnt, sink);
-      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf};
+      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf, sink.okmask};
       sp.lanes[li] = L;
       ++rewalks;
     }
@@ -488,6 +562,7 @@ __device__ void resolve_group(const SparseParams &sp, uint32_t w, Seg s, uint32_
   Seg a = lane_seg(sp, l0, sp.lanes[l0]);
   for (uint32_t j = 1; j < size; ++j) a = sp_cat(sp, a, lane_seg(sp, l0 + j, sp.lanes[l0 + j]));
   put_seg(sp.aggs + (uint64_t)w * kSparseAggWords, a);
+  put_lite(sp, w, a);
 }
 
 __device__ __forceinline__ void fence_agent() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
@@ -497,6 +572,16 @@ __device__ __forceinline__ void fence_agent() { __builtin_amdgcn_fence(__ATOMIC_
 // inside): runs of plainly linked groups compose by sums
 __device__ __forceinline__ bool plain_link(const SparseParams &sp, const Seg &p, const Seg &a) {
   return a.valid && p.exit >= sp_end(sp, p.last) && p.exit < sp_end(sp, a.last) && p.exit == a.entry;
+}
+// the fields of a group aggregate the fast path reads
+struct Lite {
+  uint64_t entry, exit, cnt, ok;
+  int64_t last;
+  uint32_t valid;
+};
+__device__ __forceinline__ bool plain_lite(const SparseParams &sp, const Lite &p, const Lite &a) {
+  const bool v = a.valid != 0, live = p.exit >= sp_end(sp, p.last), in = p.exit < sp_end(sp, a.last);
+  return v && live && in && p.exit == a.entry;
 }
 __device__ __forceinline__ int64_t group_last_lane(const SparseParams &sp, uint64_t w) {
   const uint64_t l = (w + 1) * 64;
@@ -556,6 +641,7 @@ struct RunInfo {       // a run of plainly linked groups [s, e): the chain state
 
 __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
   __shared__ uint64_t wsc[kScanThreads / 64 + 1], wso[kScanThreads / 64 + 1];
+  __shared__ uint64_t s_en[kScanWin], s_ex[kScanWin + 1], s_co[kScanWin];  // the fast path's staged link fields
   __shared__ uint32_t wsn[kScanThreads / 64 + 1];
   __shared__ Seg badx[kResolvers];
   __shared__ uint32_t bad[kResolvers];
@@ -608,6 +694,77 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
   }
   __syncthreads();
   if (fail) return;  // no summary: npr_dev_check reports the previous link's failure as a timeout
+  // Fast path (C3: the anchor and every group link plainly, one run): each group's incoming state
+  // is its predecessor's exit and two sums.  The link fields are staged in LDS kScanWin groups at a
+  // time by coalesced loads; each thread then takes kScanWin / kScanThreads consecutive groups.
+  {
+    const Seg E = E0;
+    uint64_t carry_c = E.cnt, carry_o = E.ok;
+    bool linked = true;
+    for (uint32_t v0 = 0; v0 < W; v0 += kScanWin) {
+      const uint32_t nw = W - v0 < kScanWin ? W - v0 : kScanWin;
+      {  // every load in flight before the first LDS store (a loop would wait for each in turn)
+        constexpr uint32_t kPer = kScanWin / kScanThreads;
+        uint64_t en[kPer], ex[kPer], co[kPer];
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+          const uint32_t i = tid + u * kScanThreads, ii = i < nw ? i : 0u;
+          en[u] = sp.lite[v0 + ii];
+          ex[u] = sp.lite[W + v0 + ii];
+          co[u] = sp.lite[2 * (uint64_t)W + v0 + ii];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kPer; ++u) {
+          const uint32_t i = tid + u * kScanThreads;
+          if (i < nw) {
+            s_en[i] = en[u];
+            s_ex[i + 1] = ex[u];
+            s_co[i] = co[u];
+          }
+        }
+      }
+      if (tid == 0) s_ex[0] = v0 ? sp.lite[W + v0 - 1] : E.exit;
+      __syncthreads();
+      constexpr uint32_t kPer = kScanWin / kScanThreads;
+      const uint32_t i0 = tid * kPer, i1 = i0 + kPer < nw ? i0 + kPer : nw;
+      uint64_t c = 0, o = 0;
+      for (uint32_t i = i0; i < i1; ++i) {
+        const uint32_t w = v0 + i;
+        const uint64_t co = s_co[i];
+        const Lite pr{0, s_ex[i], 0, 0, w ? group_last_lane(sp, w - 1) : E.last, 1};
+        const Lite a{s_en[i], s_ex[i + 1], co & 0xffffffffull, (co >> 32) & 0x7fffffffull, group_last_lane(sp, w),
+                     (uint32_t)(co >> 63)};
+        linked = linked && plain_lite(sp, pr, a);
+        c += a.cnt;
+        o += a.ok;
+      }
+      uint64_t tc, to;
+      uint32_t n = 0, tn;
+      block_scan3(c, o, n, tc, to, tn, wsc, wso, wsn);
+      for (uint32_t i = i0; i < i1; ++i) {
+        const uint64_t co = s_co[i];
+        sp.pre[v0 + i] = SparsePre{s_ex[i], carry_c + c, carry_o + o, 0};
+        c += co & 0xffffffffull;
+        o += (co >> 32) & 0x7fffffffull;
+      }
+      carry_c += tc;
+      carry_o += to;
+      __syncthreads();
+    }
+    if (__syncthreads_and(linked ? 1 : 0)) {
+      if (tid == 0) {
+        npr_summary *sm = kp.summary;
+        sm->n_records = carry_c;
+        sm->n_flows = carry_o;
+        sm->consumed = W ? sp.lite[W + W - 1] : E.exit;
+        sm->flags = (kp.flows && carry_o > kp.flow_cap) ? NPR_SUMMARY_FLOW_OVERFLOW : 0u;
+        sm->epoch = kp.epoch;
+        sm->entry = entry0;
+        __hip_atomic_store(sp.ctl, gran(kp.epoch, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+  }
   for (uint32_t round = 0;; ++round) {
     // every round settles the lowest contradicted group for good: more rounds than groups is a bug,
     // and the launch then ends without a summary (npr_dev_check reports it) instead of spinning
@@ -734,15 +891,18 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
 
 // =============================================================================================
 // k_sparse_rows: group w's Ok flows (file order i = 0 .. okw-1, global index O + i) to rows
-// flow_cap - 1 - (O + i); thread b writes the b-th row of the group's block, so consecutive
-// threads store consecutive rows
+// flow_cap - 1 - (O + i).  The group's slots go through LDS kRowChunk slot rows at a time: read
+// as 1-KiB contiguous pieces, written back as each lane's run of consecutive rows (thread 4j + s
+// takes lane j's slots k0 + s + 4m: the four threads of a lane store neighbouring rows).
 // =============================================================================================
+constexpr uint32_t kRowChunk = 16;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
 __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   __shared__ uint32_t opre[65];
-  __shared__ uint32_t okl[64];
-  __shared__ uint64_t ovf[64], hil[64];
+  __shared__ uint32_t okl[64], sl[64];  // Ok flows of the lane, in its slots
+  __shared__ uint64_t ovf[64], hil[64], msk[64];
+  __shared__ uint32_t kmax_sh;
   __shared__ SparseLane ls[64];
-  __shared__ uint32_t rows[64 * kSpRow];
+  __shared__ __attribute__((aligned(16))) u32x4 stage[kRowChunk * 64 * 2];
   const ParseParams &kp = sp.kp;
   const uint32_t w = blockIdx.x, tid = threadIdx.x;
   if (__hip_atomic_load(sp.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gran(kp.epoch, 1)) return;
@@ -754,15 +914,20 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   if (tid == 0) {  // which lanes the exact chain runs through (every link is consistent now)
     uint64_t s = P.exit;
     bool ended = s < sp_end(sp, (int64_t)l0 - 1);
-    uint32_t acc = 0;
+    uint32_t acc = 0, km = 0;
     for (uint32_t j = 0; j < 64; ++j) {
       opre[j] = acc;
       okl[j] = 0;
+      sl[j] = 0;
+      msk[j] = 0;
       if (j >= size || ended) continue;
       const uint64_t hi = sp_end(sp, (int64_t)(l0 + j));
       if (s >= hi) continue;  // a record spans the lane
       const SparseLane &L = ls[j];
       okl[j] = L.ok;
+      msk[j] = L.okmask;
+      sl[j] = (uint32_t)__builtin_popcountll(L.okmask);
+      if (L.okmask) km = max(km, 64u - (uint32_t)__builtin_clzll(L.okmask));
       ovf[j] = L.ovf;
       hil[j] = hi;
       acc += L.ok;
@@ -770,27 +935,49 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
       ended = s < hi;
     }
     opre[64] = acc;
+    kmax_sh = km;
   }
   __syncthreads();
-  const uint32_t okw = opre[64];
+  const uint32_t kmax = kmax_sh;
   const uint64_t O = P.ok;
-  for (uint32_t b = tid; b < okw; b += kSpBlock) {
-    const uint32_t i = okw - 1 - b;
-    const uint64_t gi = O + i;
-    if (gi >= kp.flow_cap) continue;
-    uint32_t j = 0;  // the lane of flow i: the last j with opre[j] <= i
+  const u32x4 *area = reinterpret_cast<const u32x4 *>(sp.area) + (uint64_t)w * sp.cap * 128u;
+  const uint32_t j = tid >> 2, sub = tid & 3u;
+  const uint64_t mj = msk[j];
+  const uint32_t pj = opre[j];
+  for (uint32_t k0 = 0; k0 < kmax; k0 += kRowChunk) {
+    const uint32_t nk = kmax - k0 < kRowChunk ? kmax - k0 : kRowChunk;
+    {  // every slot load in flight before the first LDS store
+      constexpr uint32_t kPer = kRowChunk * 128u / kSpBlock;
+      u32x4 v[kPer];
 #pragma unroll
-    for (uint32_t step = 32; step; step >>= 1)
-      if (opre[j + step] <= i) j += step;
-    const uint32_t r = i - opre[j];
-    if (r >= sp.cap) continue;  // past the lane's slots: its overflow walk below
-    const u32x4 *src = reinterpret_cast<const u32x4 *>(sp.area + (((uint64_t)w * sp.cap + r) * 64u + j) * 8u);
-    put_row(kp, kp.flow_cap - 1 - gi, src[0], src[1]);
+      for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t q = tid + u * kSpBlock;
+        v[u] = area[(uint64_t)k0 * 128u + (q < nk * 128u ? q : 0u)];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kPer; ++u) {
+        const uint32_t q = tid + u * kSpBlock;
+        if (q < nk * 128u) stage[q] = v[u];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t m = 0; m < kRowChunk / 4; ++m) {
+      const uint32_t k = k0 + sub + 4 * m;
+      if (k < k0 + nk && ((mj >> k) & 1ull)) {
+        const uint64_t gi = O + pj + (uint32_t)__builtin_popcountll(mj & ((1ull << k) - 1ull));
+        if (gi < kp.flow_cap) {
+          const uint32_t q = ((k - k0) * 64u + j) * 2u;
+          put_row(kp, kp.flow_cap - 1 - gi, stage[q], stage[q + 1]);
+        }
+      }
+    }
+    __syncthreads();
   }
-  if (tid < 64 && okl[tid] > sp.cap) {  // a lane with more Ok flows than slots: the rest walked again
-    RowSink sink{&kp, O + opre[tid], sp.cap};
+  if (tid < 64 && okl[tid] > sl[tid]) {  // Ok flows past the lane's slots: walked again from its first slotless record
+    RowSink sink{&kp, O + opre[tid], sl[tid]};
     uint32_t cnt = 0;
-    (void)lane_walk(kp, rows + tid * kSpRow, ovf[tid], hil[tid], cnt, sink);
+    (void)lane_walk(kp, reinterpret_cast<uint32_t *>(stage) + tid * kSpRow, ovf[tid], hil[tid], cnt, sink);
   }
 }
 
