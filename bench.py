@@ -300,19 +300,26 @@ def run_sharded(args, dev, local, rank, world):
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     # C4 frames are IPv4 by construction: no IPv6 side table to move (pass ws.flows_v6 rows otherwise)
-    # the per-step 64-B summaries are exchanged on the host (gloo over loopback: one node), off the
-    # GPU timeline; without gloo the same step all-gathers them over RCCL between two parses
+    # the per-step 64-B summaries are exchanged on the host, off the GPU timeline: through node-local
+    # shared memory (parallel.ShmExchange, ~40 us at 8 ranks), else gloo over loopback (~1.4 ms at 8
+    # ranks), else an RCCL all-gather of the device summaries between two parses
     os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
     try:
         meta = dist.new_group(backend="gloo")
     except RuntimeError as e:
         print(f"[rank {rank}] no gloo group ({e}); summaries over RCCL", file=sys.stderr, flush=True)
         meta = None
-    # eight steps in flight; the oldest four are finished by ONE host exchange, so an all-gather over
-    # loopback that is slower than a parse (gloo, 8 ranks) is paid once per four parses
+    xchg = None
+    if meta is not None:
+        try:
+            xchg = parallel.ShmExchange(meta)
+        except RuntimeError as e:
+            print(f"[rank {rank}] no shared-memory exchange ({e}); summaries over gloo", file=sys.stderr, flush=True)
+    # eight steps in flight, the oldest four finished by ONE host exchange (so a slow exchange, gloo at
+    # 8 ranks, is paid once per four parses)
     depth = 8
     step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000,
-                                       meta_group=meta, depth=depth)
+                                       meta_group=meta, depth=depth, exchange=xchg)
     metas, live, rounds = step.step()
     _, _, r_tot, f_tot = parallel.prefix_offsets(metas, live)
     assert rounds == 1 and r_tot == n_total and f_tot == n_total, (rounds, r_tot, f_tot)
@@ -369,7 +376,8 @@ def run_sharded(args, dev, local, rank, world):
     out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
     out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
     step_ms = wall * 1e3 / args.steps
-    out["exchange"] = {"collective": ("all-gather of the ranks' 64-B parse summaries on the host (gloo), one per "
+    how = ("node-local shared memory (npr_shm_all_gather)" if xchg is not None else "gloo over loopback")
+    out["exchange"] = {"collective": (f"all-gather of the ranks' 64-B parse summaries on the host ({how}), one per "
                                       f"{depth // 2} steps ({depth} in flight), overlapped with the later steps' parses; RCCL "
                                       "carries the flow rows") if meta is not None
                        else "RCCL all_gather of the ranks' device summaries, one per step", "rounds": rounds}

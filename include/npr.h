@@ -461,6 +461,17 @@ npr_status npr_dev_convert_records(npr_ctx *ctx, const void *input, uint64_t len
                                    const npr_record *records, uint64_t n, npr_flow *out,
                                    npr_flow_v6 *out_v6, uint64_t cap, uint64_t *n_out, void *stream);
 
+/* ---- multi-GPU runtime (no reference counterpart) ------------------------------------------- */
+/* The per-step summary exchange of the multi-GPU step on ONE node: `seg` is a
+ * mapping, shared by the `world` rank processes, of world x depth slots of `rec` bytes each (slot
+ * (r, d) at byte (r * depth + d) * rec: an 8-byte sequence word, the payload from byte 64).  Rank
+ * `rank` publishes `mine` (n bytes) as exchange number `seq` (1, 2, ... in every rank's call
+ * order) in its slot seq % depth, then waits until every rank's slot holds exchange `seq` and
+ * copies the world payloads to out[world][n].  Spins, then yields; NPR_ERR_TIMEOUT after
+ * timeout_ms.  depth >= 2: a slot is rewritten only after every rank has read it. */
+npr_status npr_shm_all_gather(void *seg, int world, int rank, int depth, uint64_t rec, uint64_t seq,
+                              const void *mine, uint64_t n, void *out, int timeout_ms);
+
 #ifdef __cplusplus
 }
 #endif

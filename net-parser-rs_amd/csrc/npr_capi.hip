@@ -4,8 +4,10 @@
 // on the CPU by design; every multi-record path runs on the device.  There is no CPU fallback:
 // without a HIP device npr_ctx_create fails.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1354,6 +1356,44 @@ npr_status npr_parse_extract_pipelined(npr_ctx *c, const uint8_t *in, size_t len
   if (n_flows) *n_flows = fin.n_flows;
   if (consumed) *consumed = fin.consumed;
   if (fin.n_flows > flow_cap || fin.flags) return fail(c, NPR_ERR_CAPACITY, "output capacity exceeded");
+  return NPR_OK;
+}
+
+// ---- the multi-GPU step's node-local summary exchange (parallel.ShmExchange) -------------------
+npr_status npr_shm_all_gather(void *seg, int world, int rank, int depth, uint64_t rec, uint64_t seq,
+                              const void *mine, uint64_t n, void *out, int timeout_ms) {
+  if (!seg || world <= 0 || rank < 0 || rank >= world || depth < 2 || rec < 64 + n || !seq || (n && (!mine || !out)))
+    return NPR_ERR_ARG;
+  uint8_t *base = (uint8_t *)seg;
+  const uint64_t d = seq % (uint64_t)depth;
+  uint8_t *my = base + ((uint64_t)rank * depth + d) * rec;
+  memcpy(my + 64, mine, n);
+  __atomic_store_n((uint64_t *)my, seq, __ATOMIC_RELEASE);  // the payload before the sequence word
+  timespec t0{};
+  bool timed = false;
+  for (int r = 0; r < world; ++r) {
+    const uint8_t *sl = base + ((uint64_t)r * depth + d) * rec;
+    for (uint32_t spins = 0; __atomic_load_n((const uint64_t *)sl, __ATOMIC_ACQUIRE) != seq; ++spins) {
+      if (spins < 512) {
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+        continue;
+      }
+      sched_yield();  // ranks may share host cores
+      if ((spins & 255u) == 0) {
+        timespec t;
+        clock_gettime(CLOCK_MONOTONIC, &t);
+        if (!timed) {
+          t0 = t;
+          timed = true;
+        } else if ((t.tv_sec - t0.tv_sec) * 1000 + (t.tv_nsec - t0.tv_nsec) / 1000000 > timeout_ms) {
+          return NPR_ERR_TIMEOUT;
+        }
+      }
+    }
+    memcpy((uint8_t *)out + (uint64_t)r * n, sl + 64, n);
+  }
   return NPR_OK;
 }
 

@@ -368,20 +368,28 @@ __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 
 }
 // every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
 // wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded
+// 16-B store with a cache policy (timing variants: 0 plain write-back, 1 non-temporal, 2 write-
+// through sc1, 3 sc0 sc1)
+template <int POL>
+__device__ __forceinline__ void store16(u32x4 *d, u32x4 v) {
+  if constexpr (POL == 1) {
+    __builtin_nontemporal_store(v, d);
+  } else if constexpr (POL == 2) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
+  } else if constexpr (POL == 3) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d), "v"(v) : "memory");
+  } else {
+    *d = v;
+  }
+}
 #ifndef NPR_SP_SLOT_POLICY
 #define NPR_SP_SLOT_POLICY 0
 #endif
-__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) {
-#if NPR_SP_SLOT_POLICY == 1
-  __builtin_nontemporal_store(v, d);
-#elif NPR_SP_SLOT_POLICY == 2
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
-#elif NPR_SP_SLOT_POLICY == 3
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d), "v"(v) : "memory");
-#else
-  *d = v;
+#ifndef NPR_SP_ROW_POLICY
+#define NPR_SP_ROW_POLICY 0
 #endif
-}
+__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) { store16<NPR_SP_SLOT_POLICY>(d, v); }
+__device__ __forceinline__ void row_store(u32x4 *d, u32x4 v) { store16<NPR_SP_ROW_POLICY>(d, v); }
 struct AreaSink {
   u32x4 *slot0;  // the lane's slot 0 (its first 16 B); NULL: count only
   uint32_t cap, n, okn;
@@ -411,8 +419,8 @@ __device__ __forceinline__ u32x4 *slot_base(const SparseParams &sp, uint64_t g, 
 __device__ __forceinline__ void put_row(const ParseParams &kp, uint64_t o, u32x4 s0, u32x4 s1) {
   const bool v6 = (s1[2] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
   u32x4 *d = reinterpret_cast<u32x4 *>(kp.flows + o * 8);
-  d[0] = u32x4{v6 ? 0u : s0[0], s0[1], s0[2], s0[3]};
-  d[1] = s1;
+  row_store(d, u32x4{v6 ? 0u : s0[0], s0[1], s0[2], s0[3]});
+  row_store(d + 1, s1);
   if (v6 && kp.flows_v6) {
     const uint64_t p = (uint64_t)(s1[2] >> 24) | ((uint64_t)s1[3] << 8);
     const uint8_t *end = kp.buf + kp.len, *a = kp.buf + p + 16 + s0[0];
@@ -895,7 +903,10 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
 // as 1-KiB contiguous pieces, written back as each lane's run of consecutive rows (thread 4j + s
 // takes lane j's slots k0 + s + 4m: the four threads of a lane store neighbouring rows).
 // =============================================================================================
-constexpr uint32_t kRowChunk = 16;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
+#ifndef NPR_SP_ROW_CHUNK
+#define NPR_SP_ROW_CHUNK 16
+#endif
+constexpr uint32_t kRowChunk = NPR_SP_ROW_CHUNK;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
 __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   __shared__ uint32_t opre[65];
   __shared__ uint32_t okl[64], sl[64];  // Ok flows of the lane, in its slots

@@ -115,7 +115,7 @@ EXPORTED = [
     "npr_dev_parse_extract", "npr_dev_parse_extract_range", "npr_dev_parse_extract_chain",
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
-    "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch",
+    "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch", "npr_shm_all_gather",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -176,6 +176,8 @@ _SIGNATURES = {
     "npr_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
     "npr_dev_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "npr_dev_parse_extract_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+    "npr_shm_all_gather": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                          ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
 }
 
 _lib = None

@@ -281,6 +281,112 @@ def shard_local(ws, buf, base, file_len, endianness=_abi.LITTLE, usec_magic=True
     return local
 
 
+class GlooExchange:
+    """The per-step summaries' all-gather over a gloo group (TCP over loopback on one node)."""
+
+    def __init__(self, group):
+        import torch.distributed as dist
+        self.group, self.world = group, dist.get_world_size(group)
+
+    def all_gather(self, mine):
+        """mine: the same number of bytes on every rank (a CPU uint8 tensor) -> (world, n) uint8."""
+        import torch
+        import torch.distributed as dist
+        out = torch.empty(self.world * mine.numel(), dtype=torch.uint8)
+        dist.all_gather(list(out.view(self.world, -1).unbind(0)), mine.contiguous(), group=self.group)
+        return out.view(self.world, -1)
+
+
+class ShmExchange:
+    """The per-step summaries' all-gather through node-local shared memory: every
+    rank process of one node maps one segment; rank r publishes step k's bytes in its slot
+    k mod depth (payload first, then the sequence number k in the slot's own cache line) and reads
+    every rank's slot once its sequence number is k.  No socket, no kernel, no collective call:
+    ~tens of microseconds where the gloo all-gather over loopback took 0.3 ms at 2 ranks and 1.3 ms
+    at 8 (this container).  A slot is rewritten only depth >= 2 exchanges later, after every rank
+    has read it (a rank writes step k + 1 only after reading all of step k).  x86 stores are seen
+    in program order, so a reader that sees k sees k's payload.
+    Built over a process group only to agree on the segment's name (all ranks on one host)."""
+
+    HEADER = 64  # the sequence number's own cache line, then the payload
+
+    def __init__(self, group=None, slot_bytes=1024, depth=4, directory="/dev/shm", timeout_s=120.0):
+        import os
+        import socket
+        import uuid
+        import torch.distributed as dist
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        hosts = [None] * self.world
+        dist.all_gather_object(hosts, socket.gethostname(), group=group)
+        if len(set(hosts)) != 1:
+            raise RuntimeError(f"ShmExchange: the ranks are on more than one host ({sorted(set(hosts))})")
+        name = [f"npr_xchg_{os.getpid()}_{uuid.uuid4().hex}" if self.rank == 0 else None]
+        src = dist.get_global_rank(group, 0) if group is not None else 0
+        dist.broadcast_object_list(name, src=src, group=group)
+        path = os.path.join(directory, name[0])
+        self.slot_bytes, self.depth, self.timeout_s = int(slot_bytes), max(2, int(depth)), float(timeout_s)
+        self.rec = (self.HEADER + self.slot_bytes + 63) // 64 * 64
+        size = self.world * self.depth * self.rec
+        ok = [True]
+        if self.rank == 0:
+            try:
+                with open(path, "wb") as f:
+                    f.truncate(size)
+            except OSError:
+                ok = [False]
+        dist.broadcast_object_list(ok, src=src, group=group)
+        if not ok[0]:
+            raise RuntimeError(f"ShmExchange: cannot create {path}")
+        try:
+            self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(size,))
+        finally:
+            dist.barrier(group=group)  # every rank mapped (or failed): the name is no longer needed
+            if self.rank == 0:
+                os.unlink(path)
+        grid = self.mm.reshape(self.world, self.depth, self.rec)
+        self.seqs = grid.view(np.uint64)[:, :, 0]  # [rank, slot]: the slot's sequence number
+        self.pay = grid[:, :, self.HEADER:]         # [rank, slot, byte]
+        self.seq = 0
+        try:  # the spin in C (npr_shm_all_gather: acquire / release atomics); numpy otherwise
+            self.lib = _abi.load_library()
+        except (ImportError, OSError):
+            self.lib = None
+
+    def all_gather(self, mine):
+        """mine: the same number (<= slot_bytes) of bytes on every rank -> (world, n) uint8 tensor."""
+        import time
+        import torch
+        a = (mine.numpy() if hasattr(mine, "numpy") else np.asarray(mine)).view(np.uint8).reshape(-1)
+        n = a.size
+        if n > self.slot_bytes:
+            raise ValueError(f"ShmExchange: {n} bytes > slot of {self.slot_bytes}")
+        self.seq += 1
+        if self.lib is not None:
+            a = np.ascontiguousarray(a)
+            out = np.empty((self.world, n), dtype=np.uint8)
+            st = self.lib.npr_shm_all_gather(self.mm.ctypes.data, self.world, self.rank, self.depth, self.rec, self.seq,
+                                             a.ctypes.data, n, out.ctypes.data, int(self.timeout_s * 1000))
+            if st != _abi.OK:
+                raise RuntimeError(f"ShmExchange: exchange {self.seq} failed (status {st}: a rank did not publish)")
+            return torch.from_numpy(out)
+        d = self.seq % self.depth
+        self.pay[self.rank, d, :n] = a
+        self.seqs[self.rank, d] = self.seq  # published after the payload
+        col = self.seqs[:, d]
+        spins, t0 = 0, None
+        while not (col == self.seq).all():
+            spins += 1
+            if spins > 64:
+                time.sleep(0)  # yield: ranks may share host cores
+                if t0 is None:
+                    t0 = time.monotonic()
+                elif time.monotonic() - t0 > self.timeout_s:
+                    late = [int(r) for r in np.nonzero(col != self.seq)[0]]
+                    raise RuntimeError(f"ShmExchange: ranks {late} did not publish step {self.seq}")
+        return torch.from_numpy(np.ascontiguousarray(self.pay[:, d, :n]))
+
+
 def record_range_shards(n_records, world, record_bytes=80, header=24):
     """C4 layout: a fixed-stride capture of n_records split by record range, rank g
     holding records [g*R, (g+1)*R): returns per rank (base, start, stop, speculative) in file
@@ -307,7 +413,7 @@ class DeviceShardedParse:
     [base, base + nbytes)."""
 
     def __init__(self, ws, buf, base, bounds, file_len, endianness=_abi.LITTLE, usec_magic=True, ts_ref=None,
-                 start=24, group=None, nbytes=None, chunk_bytes=0, meta_group=None, depth=2):
+                 start=24, group=None, nbytes=None, chunk_bytes=0, meta_group=None, depth=2, exchange=None):
         import torch
         import torch.distributed as dist
         self.ws, self.buf, self.base, self.bounds = ws, buf, int(base), bounds
@@ -326,21 +432,26 @@ class DeviceShardedParse:
         self._ev2 = [torch.cuda.Event() if pin else None for _ in range(self.depth)]
         self._k = 0
         self.pending = []
-        # meta_group (a gloo group over the same ranks): launch_step's exchange moves the 64-B
-        # summaries on the HOST instead (D2H on a side stream, all-gathered in finish_step), so no
-        # collective kernel or stream join sits between two parses; the flow rows still go over RCCL
+        # exchange (ShmExchange: node-local shared memory) or meta_group (a gloo group over the same
+        # ranks): the 64-B summaries move on the HOST (the parse stores its summary into page-locked
+        # host memory, all-gathered in finish_steps), so no collective kernel or stream join sits
+        # between two parses; the flow rows still go over RCCL
         self.meta_group = meta_group
+        self.xchg = exchange if exchange is not None else (GlooExchange(meta_group) if meta_group is not None else None)
         # every rank's buffer end, once: a chain that stops short of its shard's stop inside a buffer
         # that does not reach the file's end is a HaloError, and every rank must decide it alike
         # (the others would otherwise wait in their next collective for the rank that raised)
-        grp = meta_group if meta_group is not None else group
-        on_host = dist.get_backend(grp) == "gloo"
-        dev = torch.device("cpu") if on_host else ws.summary.device
-        mine = torch.tensor([self.base + self.nbytes], dtype=torch.int64, device=dev)
-        ends = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
-        dist.all_gather(ends, mine, group=grp)
-        self.buf_ends = [int(e.item()) for e in ends]
-        if meta_group is not None:
+        if self.xchg is not None:
+            mine = torch.tensor([self.base + self.nbytes], dtype=torch.int64)
+            self.buf_ends = [int(x) for x in self.xchg.all_gather(mine.view(torch.uint8)).view(torch.int64).reshape(-1)]
+        else:
+            on_host = dist.get_backend(group) == "gloo"
+            dev = torch.device("cpu") if on_host else ws.summary.device
+            mine = torch.tensor([self.base + self.nbytes], dtype=torch.int64, device=dev)
+            ends = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(self.world)]
+            dist.all_gather(ends, mine, group=group)
+            self.buf_ends = [int(e.item()) for e in ends]
+        if self.xchg is not None:
             # the parse's last link stores its summary straight into page-locked host memory: the
             # host waits for an event behind the parse, no copy kernel needs a CU the next parse holds
             self._sum2 = [torch.zeros(ws.summary.numel(), dtype=torch.uint8, pin_memory=pin) for _ in range(self.depth)]
@@ -393,11 +504,10 @@ class DeviceShardedParse:
     def _exchange(self):
         import torch
         import torch.distributed as dist
-        if self.meta_group is not None:  # the summary is in host memory: wait for the parse, gather on the host
+        if self.xchg is not None:  # the summary is in host memory: wait for the parse, gather on the host
             if torch.cuda.is_available():
                 torch.cuda.current_stream().synchronize()
-            dist.all_gather(list(self._gh.view(self.world, -1).unbind(0)), self.ws.summary, group=self.meta_group)
-            return self._metas(self._gh)
+            return self._metas(self.xchg.all_gather(self.ws.summary).reshape(-1))
         dist.all_gather_into_tensor(self.gathered, self.ws.summary, group=self.group)
         return self._metas(self.gathered.cpu())
 
@@ -413,7 +523,7 @@ class DeviceShardedParse:
         lo, hi = self.bounds[self.rank]
         i = self._k % self.depth
         self._k += 1
-        if self.meta_group is not None:
+        if self.xchg is not None:
             self._bind(self._sum2[i])
             self._launch(self.start if self.rank == 0 else lo, self.rank > 0)
             if self._ev2[i] is not None:
@@ -446,12 +556,10 @@ class DeviceShardedParse:
         for i in slots:
             if self._ev2[i] is not None:
                 self._ev2[i].synchronize()
-        if self.meta_group is not None:  # the summaries' all-gather on the host (gloo), all n steps at once
+        if self.xchg is not None:  # the summaries' all-gather on the host, all n steps at once
             sn = self._sum2[0].numel()
             mine = torch.cat([self._sum2[i] for i in slots])
-            out = torch.empty(self.world * n * sn, dtype=torch.uint8)
-            dist.all_gather(list(out.view(self.world, -1).unbind(0)), mine, group=self.meta_group)
-            per = out.view(self.world, n, sn)
+            per = self.xchg.all_gather(mine).view(self.world, n, sn)
             for j, i in enumerate(slots):
                 self._h2[i].copy_(per[:, j, :].reshape(-1))
         res = None

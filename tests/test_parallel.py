@@ -226,8 +226,10 @@ def _step_rank_main(rank, world, port, blob, wrong, q, pipelined=False):
         spec = spec_off_by(recs, 1) if wrong else spec_exact(recs)
         ws = OracleShardWorkspace(len(recs) + 1, spec)
         meta = dist.new_group(backend="gloo") if str(pipelined).startswith("host_meta") else None
-        deep = pipelined == "host_meta_d4"
-        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), meta_group=meta, depth=4 if deep else 2)
+        xchg = parallel.ShmExchange() if str(pipelined).startswith("shm") else None
+        deep = pipelined in ("host_meta_d4", "shm_d4")
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), meta_group=meta, depth=4 if deep else 2,
+                                           exchange=xchg)
         if deep:  # the bench's N > 1 loop: four steps in flight, the oldest two finished by ONE exchange
             rounds = 0
             for _ in range(7):
@@ -261,8 +263,8 @@ def _step_rank_main(rank, world, port, blob, wrong, q, pipelined=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipelined", [False, True, "host_meta", "host_meta_d4"],
-                         ids=["step", "launch_finish", "host_meta", "host_meta_depth4"])
+@pytest.mark.parametrize("pipelined", [False, True, "host_meta", "host_meta_d4", "shm", "shm_d4"],
+                         ids=["step", "launch_finish", "host_meta", "host_meta_depth4", "shm", "shm_depth4"])
 @pytest.mark.parametrize("wrong", [False, True], ids=["exact", "rerun"])
 def test_gloo_world2_device_step_protocol(wrong, pipelined):
     """DeviceShardedParse (the bench's multi-GPU step) + gather_flow_tables over gloo: each rank holds
@@ -330,7 +332,7 @@ def spanning_capture():
     return a + jumbo + b
 
 
-def _span_rank_main(rank, world, port, blob, q):
+def _span_rank_main(rank, world, port, blob, q, shm=False):
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -342,7 +344,8 @@ def _span_rank_main(rank, world, port, blob, q):
         shard = torch.from_numpy(np.frombuffer(blob[base:], dtype=np.uint8).copy())
         # rank 1's speculation finds no record start (there is none): its first byte is the guess
         ws = OracleShardWorkspace(len(recs) + 1, spec_exact(recs))
-        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob),
+                                           exchange=parallel.ShmExchange() if shm else None)
         metas, live, rounds = step.step()
         fl, f6 = step.rows()
         merged, _ = parallel.gather_flow_tables(fl, None, metas, live)
@@ -352,7 +355,8 @@ def _span_rank_main(rank, world, port, blob, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world3_record_spans_a_whole_shard():
+@pytest.mark.parametrize("shm", [False, True], ids=["gloo", "shm"])
+def test_gloo_world3_record_spans_a_whole_shard(shm):
     blob = spanning_capture()
     bounds = parallel.shard_bounds(24, len(blob), 3)
     _, recs, _, _ = full_reference(blob)
@@ -361,7 +365,7 @@ def test_gloo_world3_record_spans_a_whole_shard():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_span_rank_main, args=(r, 3, port, blob, q)) for r in range(3)]
+    procs = [ctx.Process(target=_span_rank_main, args=(r, 3, port, blob, q, shm)) for r in range(3)]
     for p in procs:
         p.start()
     for p in procs:
@@ -372,7 +376,7 @@ def test_gloo_world3_record_spans_a_whole_shard():
 
 
 # ---- a short halo: every rank raises HaloError together ------------------------------------------
-def _halo_rank_main(rank, world, port, blob, q):
+def _halo_rank_main(rank, world, port, blob, q, shm=False):
     import torch
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -385,7 +389,8 @@ def _halo_rank_main(rank, world, port, blob, q):
         end = hi - 10 if rank == 0 else len(blob)
         shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
         ws = OracleShardWorkspace(len(recs) + 1, spec_exact(recs))
-        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob))
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob),
+                                           exchange=parallel.ShmExchange() if shm else None)
         try:
             step.step()
             q.put((rank, "no error"))
@@ -395,7 +400,8 @@ def _halo_rank_main(rank, world, port, blob, q):
         dist.destroy_process_group()
 
 
-def test_gloo_world2_short_halo_raises_on_every_rank():
+@pytest.mark.parametrize("shm", [False, True], ids=["gloo", "shm"])
+def test_gloo_world2_short_halo_raises_on_every_rank(shm):
     """A rank whose buffer stops inside a record before its shard's stop: HaloError on BOTH ranks
     (decided from the shared summaries and buffer ends), so no rank goes on into a collective the
     raising rank never joins."""
@@ -403,7 +409,7 @@ def test_gloo_world2_short_halo_raises_on_every_rank():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_halo_rank_main, args=(r, 2, port, blob, q)) for r in range(2)]
+    procs = [ctx.Process(target=_halo_rank_main, args=(r, 2, port, blob, q, shm)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
@@ -411,3 +417,52 @@ def test_gloo_world2_short_halo_raises_on_every_rank():
         assert p.exitcode == 0
     got = sorted(q.get(timeout=10) for _ in range(2))
     assert got == [(0, "halo"), (1, "halo")]
+
+
+# ---- the summary exchange's latency at 8 ranks: node-local shared memory against gloo ------------
+def _xchg_latency_main(rank, world, port, n, q):
+    import time
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = torch.full((64,), rank, dtype=torch.uint8)
+        res = {}
+        for name, x in (("gloo", parallel.GlooExchange(None)), ("shm", parallel.ShmExchange())):
+            for _ in range(20):
+                x.all_gather(mine)
+            dist.barrier()
+            ts = []
+            for i in range(n):
+                mine[0] = i & 0xff
+                t0 = time.perf_counter()
+                out = x.all_gather(mine)
+                ts.append(time.perf_counter() - t0)
+                assert out.shape == (world, 64) and all(int(out[r, 1]) == r and int(out[r, 0]) == i & 0xff
+                                                        for r in range(world))
+            res[name] = float(np.median(ts)) * 1e6
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shm_exchange_latency_world8():
+    """the per-step summary exchange at 8 ranks (one node).  Every step all-gathers a
+    64-B summary per rank; over gloo (TCP loopback) that was 1.3 ms here, slower than one 0.23-ms
+    shard parse.  Node-local shared memory (npr_shm_all_gather): 36-44 us median on this 8-CPU
+    container, where pytest and the 8 ranks share the cores (the bound below leaves room for that
+    noise)."""
+    world, n = 8, 300
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xchg_latency_main, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+        assert p.exitcode == 0
+    res = q.get(timeout=10)
+    print(f"median all-gather of 64 B at {world} ranks: shm {res['shm']:.1f} us, gloo {res['gloo']:.1f} us")
+    assert res["shm"] < res["gloo"] / 5 and res["shm"] < 80.0, res
