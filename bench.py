@@ -142,7 +142,7 @@ def run_single(args, dev, local):
 
     # correctness gate for the measured configuration (tests/test_gpu_scale.py compares it bit for bit)
     ws.launch(bufs[0], start=24, endianness=hdr.endianness)
-    pass_ran = {1: "two-pass", 2: "resident", 4: "batched", 8: "sparse"}.get(ws.ctx.lib.npr_ctx_last_pass(ws.ctx.handle), "?")
+    pass_ran = {1: "two-pass", 2: "resident", 8: "sparse"}.get(ws.ctx.lib.npr_ctx_last_pass(ws.ctx.handle), "?")
     if args.no_gate:  # timing-only ablation builds (make ablate): their results are not checked
         torch.cuda.synchronize()
         n_flows = n
@@ -188,53 +188,10 @@ def run_single(args, dev, local):
                                    "(HIP events over the stream); stream_GBps = the capture's bytes / step time"
                                    if pass_ran == "sparse" else
                                    "C3 through the resident pass (every byte streams); achieved uses SURVEY 8d bytes")
-    if args.config == "c2" and args.batch > 1:
-        out["batched"] = batched_line(args, bufs, hdr, n, local, stream, read_b, write_b)
     if not args.no_cpu:
         sample = {"c2": "the C2 capture", "c3": "the C3 capture", "c4": "one C4 shard"}[args.config]
         out["cpu_baseline"] = cpu_baseline(blob, n, args.cpu_budget, sample)
     return out
-
-
-def batched_line(args, bufs, hdr, n, local, stream, read_b, write_b):
-    """K independent C2 captures per launch (npr_dev_parse_extract_batch, k_parse_batch): consecutive
-    capture batches of a stream, each capture's look-back and row writes overlapping the read of the
-    next one's first tiles.  Not the headline (a step there is one capture per launch); reported as
-    the per-capture time of a K-capture launch, every capture gated bit-exact like the headline."""
-    k = args.batch
-    wss = [device.Workspace(record_cap=n, flow_cap=n, device=local, records=False, offsets=False, status=False,
-                            flows=True, flows_v6=True) for _ in range(k)]
-    items = [(wss[i], bufs[i % len(bufs)], 24, hdr.endianness) for i in range(k)]
-    device.launch_batch(items, stream=stream)
-    if not args.no_gate:
-        for ws in wss:
-            sm = ws.check()
-            assert sm.n_records == n and sm.n_flows == n and sm.consumed == 24 + 80 * n, (sm.n_records, sm.n_flows)
-        # every capture's rows are the single-capture launch's (tests/test_gpu_batch.py checks the oracle)
-        for ws in wss[1:]:
-            assert torch.equal(ws.flows, wss[0].flows)
-    for _ in range(args.warmup):
-        device.launch_batch(items, stream=stream)
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        device.launch_batch(items, stream=stream)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    wall = time.perf_counter() - t0
-    launch_ms = ev0.elapsed_time(ev1) / args.steps
-    per_cap_ms = launch_ms / k
-    alg = read_b + write_b
-    return {"k": k, "captures_per_launch": k, "launch_ms": round(launch_ms, 5),
-            "per_capture_us": round(per_cap_ms * 1e3, 3),
-            "Mpackets_per_s": round(n * k * args.steps / wall / 1e6, 3),
-            "achieved_GBps": round(alg / (per_cap_ms * 1e-3) / 1e9, 1),
-            "frac": round(alg / (per_cap_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "bytes_per_capture": alg,
-            "note": ("K independent 1M x 64-B captures (the 4 resident copies in turn) parsed by ONE k_parse_batch "
-                     "launch; per-capture time = launch time / K (HIP events); every capture gated")}
 
 
 def stats_dump(ws, bufs, hdr, copies, rank):
@@ -402,8 +359,6 @@ def parse_args(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-gate", action="store_true", help=argparse.SUPPRESS)  # ablation builds only
     ap.add_argument("--stats", action="store_true", help="print speculation / hand-off counters (stderr)")
-    ap.add_argument("--batch", type=int, default=8,
-                    help="c2: also time K captures per launch (npr_dev_parse_extract_batch; the `batched` field; 1 = off)")
     ap.add_argument("--sparse-span", type=int, default=0,
                     help="c3: force the sparse record walk with lane ranges of N bytes (NPR_OPT_SPARSE N >= 64; 0 = auto)")
     ap.add_argument("--sharded", action="store_true",

@@ -206,6 +206,12 @@ int npr_abi_version(void);
 npr_status npr_ctx_create(int device, npr_ctx **out);
 void npr_ctx_destroy(npr_ctx *ctx);
 const char *npr_ctx_last_error(const npr_ctx *ctx);
+/* Call before destroying a HIP stream that was passed to any npr_dev_* call (of any context on the
+ * device).  libnpr orders the look-back launches of all contexts on a device; the order event of the
+ * last launch is recorded lazily on that launch's stream (an eager record costs ~3 us of GPU time
+ * per launch), so a destroyed stream must hand its pending record over first.  The context's own
+ * stream needs no call (npr_ctx_destroy does it). */
+npr_status npr_stream_release(npr_ctx *ctx, void *stream);
 /* Diagnostics: per-launch speculation / hand-off counters (off by default; costs atomics).
  * Counters: [0] tiles pass 2 re-walked (pass 1's entry was not the exact one), [1] prefix folds
  * that waited for a mis-speculated tile's exact prefix, [5] tiles with no plausible record
@@ -253,7 +259,7 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  * NPR_OPT_SPARSE (default 0 = auto): flows-only parses of captures of long records run the sparse
  *   record walk instead of the resident pass: lanes hop header to header and read
  *   one 112-B window per record instead of streaming every payload byte.  0 chooses it from the
- *   record density of the capture's first 256 KiB (at least 16 MiB past `start`, a known start, no
+ *   record density of the capture's first 256 KiB (at least 256 MiB past `start`, a known start, no
  *   shard); 1 never; 2 always (lane ranges sized from the density, else 16 KiB); N >= 64 always,
  *   with lane ranges of N bytes (a test knob).  Same results either way.
  * NPR_OPT_SPARSE_CAP (default 0 = 64): record slots per sparse lane; a lane with more records
@@ -263,8 +269,8 @@ enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, N
        NPR_OPT_DEVICE_WINDOW = 5, NPR_OPT_SPARSE = 6, NPR_OPT_SPARSE_CAP = 7 };
 npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
 /* Which pass the context's last device parse launch ran (tests and diagnostics; no reference
- * counterpart): 0 none yet, 1 the two-pass kernels, 2 the resident single pass, 4 a batched
- * resident launch, 8 the sparse record walk. */
+ * counterpart): 0 none yet, 1 the two-pass kernels, 2 the resident single pass, 8 the sparse
+ * record walk (4, a batched resident launch, is no longer produced). */
 int npr_ctx_last_pass(const npr_ctx *ctx);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);
@@ -392,13 +398,11 @@ typedef struct npr_shard {
 npr_status npr_dev_parse_extract_shard(npr_ctx *ctx, const void *input, uint64_t input_len,
                                        npr_endianness endianness, const npr_shard *shard,
                                        const npr_dev_outputs *out, void *stream);
-/* Several independent device-resident captures (e.g. consecutive capture batches of a stream) in ONE
- * resident launch: each item is what npr_dev_parse_extract(ctx, input, len, start, endianness, &out,
- * stream) would parse, with the same outputs and summary (check each with npr_dev_check).  The
- * workgroups take the captures in order, and each capture's prefix resolution and row writes overlap
- * the read of the next capture's first bytes; the launch's ramp and tail are paid
- * once.  Items that need more than flows (record table, offsets, status) or that one launch does not
- * hold run as their own npr_dev_parse_extract, in order. */
+/* Several independent device-resident captures (e.g. consecutive capture batches of a stream) in one
+ * call: each item is what npr_dev_parse_extract(ctx, input, len, start, endianness, &out, stream)
+ * would parse, launched in order on the stream, with the same outputs and summary (check each with
+ * npr_dev_check).  (ABI 2 ran flows-only items in one batched launch; it measured 0.96-1.09x of
+ * separate launches and was removed) */
 typedef struct npr_batch_item {
   const void *input;
   uint64_t len;
@@ -425,7 +429,10 @@ npr_status npr_flow_details(npr_ctx *ctx, const uint8_t *input, size_t len, cons
 npr_status npr_dev_flow_details(npr_ctx *ctx, const void *input, uint64_t len, const npr_record *records,
                                 uint64_t n, uint8_t *status, uint64_t *detail, void *stream);
 /* Dense extract_flow over device-resident records (device npr_record array indexing into
- * `input`; payload = input[offset+16 .. offset+16+actual_length]). */
+ * `input`; payload = input[offset+16 .. offset+16+actual_length]).  flows[i] / status[i] for every
+ * record (a failed record's flow row is zero); flows_v6[i] is written only when flows[i] is IPv6
+ * (as in the convert_records tables; the host-memory npr_extract_flows returns zero side rows for
+ * the others). */
 npr_status npr_dev_extract_flows(npr_ctx *ctx, const void *input, uint64_t len,
                                  const npr_record *records, uint64_t n, npr_flow *flows,
                                  npr_flow_v6 *flows_v6, uint8_t *status, void *stream);

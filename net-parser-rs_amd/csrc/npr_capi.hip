@@ -171,7 +171,11 @@ hipStream_t pick(npr_ctx *c, void *stream) { return stream ? (hipStream_t)stream
 
 // ---- which flows-only pass: the record density of a device capture ----------------------------
 constexpr uint64_t kProbeBytes = 256u << 10;        // walked from the known first record
-constexpr uint64_t kSparseMinBytes = 16ull << 20;   // auto: the sparse walk for ranges from this size on
+// auto: the sparse walk for ranges from this size on.  The choice costs one pinned copy and a sync
+// per capture not seen recently (~20 us): from 256 MiB on that is small against any parse of the
+// range (a 16-MiB floor made single launches of 21-MB C2-shaped captures from many buffers 52 us
+// instead of 13: scripts/bench_batch_small.py, round 4)
+constexpr uint64_t kSparseMinBytes = 256ull << 20;
 constexpr uint64_t kSparseMinMean = 384;            // ... of at least this many bytes per record (16 + incl)
 constexpr uint64_t kSparseSpanDefault = 16u << 10;  // lane range when the density is unknown
 constexpr uint64_t kSparseSpanRecords = 48;         // lane range = this many mean records (slots: 64; 24 -> 48: C3 walk 573 -> 508 us)
@@ -357,6 +361,22 @@ npr_status npr_ctx_create(int device, npr_ctx **out) {
   const char *env = getenv("NPR_RESIDENT");
   if (env && env[0] == '0') c->resident = 0;
   *out = c;
+  return NPR_OK;
+}
+
+// A caller stream is about to be destroyed: if the device's last ordered launch ran on it and its
+// order event is still pending (mode 3 records it lazily, from the next launch on another stream),
+// record it now, while the stream exists.
+npr_status npr_stream_release(npr_ctx *c, void *stream) {
+  if (!c) return NPR_ERR_ARG;
+  HIP_CHECK(c, hipSetDevice(c->device));
+  hipStream_t s = pick(c, stream);
+  DeviceOrder &o = device_order(c->device);
+  std::lock_guard<std::mutex> g(o.m);
+  if (o.pending && o.last == s) {
+    if (npr_status st = order_record(c, o, s)) return st;
+    o.pending = false;
+  }
   return NPR_OK;
 }
 
@@ -721,9 +741,9 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
     p.prev_epoch = summary_epoch(c, prev);
   }
   sp.kp = p;
+  log_summary(c, o->summary);  // before launching: a failed launch leaves the summary stale, and unclaimed
   if ((st = ordered_launch(c, s, [&] { return npr::launch_sparse(sp, s); }))) return st;
   c->last_pass = 8;
-  log_summary(c, o->summary);
   return NPR_OK;
 }
 
@@ -809,9 +829,12 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
                   (unsigned long long)nb);
     p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
   }
+  // who writes which summary (npr_dev_check and chained launches check it), logged before the launch:
+  // if the launch fails, the summary keeps an older epoch than its log entry and npr_dev_check
+  // reports it instead of returning the previous parse's results
+  log_summary(c, o->summary);
   if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_extract(p, s); }))) return st;
   c->last_pass = resident ? 2 : 1;
-  log_summary(c, o->summary);  // who wrote which summary (npr_dev_check, chained launches check it)
   return NPR_OK;
 }
 
@@ -829,78 +852,18 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   return NPR_OK;
 }
 
-// ---- K independent captures in one resident launch (k_parse_batch) ------------------------------
-// Eligible: flows-only outputs, the resident pass on, a capture one launch keeps in registers
-// (npr_dev_parse_extract would not chain it).  Anything else runs item by item.
-static bool batch_eligible(npr_ctx *c, const npr_batch_item &it) {
-  const npr_dev_outputs &o = it.out;
-  if (!c->resident || o.record_offsets || o.records || o.record_status || !o.summary) return false;
-  if (sparse_forced(c)) return false;  // every flows-only launch runs the sparse walk
-  if (!it.input || it.len <= it.start || ((uintptr_t)it.input & 15u)) return false;
-  if (o.flows && (((uintptr_t)o.flows & 15u) || (o.flows_v6 && ((uintptr_t)o.flows_v6 & 15u)))) return false;
-  if (it.len >= (1ull << 40)) return false;
-  return it.len - it.start <= (uint64_t)c->res_waves * npr::kResSlots * npr::kTile;
-}
-
-static npr_status batch_group(npr_ctx *c, const npr_batch_item *items, uint32_t n, hipStream_t s) {
-  npr::BatchParams bp{};
-  bp.n = n;
-  uint64_t off[npr::kMaxBatch + 1] = {0};
-  uint64_t nts[npr::kMaxBatch];
-  for (uint32_t k = 0; k < n; ++k) {  // slot regions: each capture's range slots, then its workgroup slots
-    npr::ParseParams &p = bp.p[k];
-    const npr_batch_item &it = items[k];
-    npr_status st = range_params(c, it.input, it.len, it.start, it.len, (npr_endianness)it.endianness, 0, it.start,
-                                 nullptr, p, nts[k]);
-    if (st) return st;
-    uint64_t wv = std::min<uint64_t>(nts[k], c->res_waves);
-    if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
-    p.nwaves = (uint32_t)wv;
-    const uint64_t nb = (wv + npr::kResWgMin - 1) / npr::kResWgMin;
-    off[k + 1] = off[k] + wv * sizeof(npr::RangeSlot) + nb * sizeof(npr::GroupSlot);
-  }
-  npr_status st = ensure(c, c->slots, off[n], true);
-  if (st) return st;
-  if ((st = next_epoch(c, s))) return st;  // one epoch for the launch: an abort stops every capture
-  for (uint32_t k = 0; k < n; ++k) {
-    npr::ParseParams &p = bp.p[k];
-    const npr_dev_outputs &o = items[k].out;
-    char *region = (char *)c->slots.p + off[k];
-    p.epoch = c->epoch;
-    p.timeout_ticks = kTimeoutTicks;
-    p.rslots = (npr::RangeSlot *)region;
-    p.rgroups = (npr::GroupSlot *)(region + (uint64_t)p.nwaves * sizeof(npr::RangeSlot));
-    p.rcnt = (uint32_t *)((char *)c->abort_word + kCtlCounters);
-    p.abort_word = c->abort_word;
-    p.flows = (uint32_t *)o.flows;
-    p.flows_v6 = (uint32_t *)o.flows_v6;
-    p.flow_cap = o.flow_cap;
-    p.summary = o.summary;
-  }
-  if ((st = ordered_launch(c, s, [&] { return npr::launch_parse_batch(bp, s); }))) return st;
-  c->last_pass = 4;
-  for (uint32_t k = 0; k < n; ++k) log_summary(c, items[k].out.summary);
-  return NPR_OK;
-}
-
+// ---- K independent captures, one call ------------------------------------------------------------
+// Each item is the ordinary npr_dev_parse_extract launch, in order on the stream.  Round 3 ran up to
+// 8 flows-only items in one resident launch (k_parse_batch); measured on 8 captures of 16 K / 64 K /
+// 262 K / 1 M records it gained 1.06x / 1.09x / 1.01x / 0.96x (profiles/r04_batch_small.jsonl), not
+// the 1.3x that would pay for a second kernel instantiation, so the entry point stays and the
+// kernel went.
 npr_status npr_dev_parse_extract_batch(npr_ctx *c, const npr_batch_item *items, uint32_t n, void *stream) {
   if (!c || (!items && n)) return fail(c, NPR_ERR_ARG, "null argument");
-  HIP_CHECK(c, hipSetDevice(c->device));
-  npr_status st = res_geometry(c);
-  if (st) return st;
-  hipStream_t s = pick(c, stream);
-  for (uint32_t i = 0; i < n;) {
-    uint32_t k = 0;
-    while (k < npr::kMaxBatch && i + k < n && batch_eligible(c, items[i + k])) ++k;
-    if (k >= 2) {
-      if ((st = batch_group(c, items + i, k, s))) return st;
-      i += k;
-    } else {  // one capture (or one that a single launch does not hold): the ordinary call
-      const npr_batch_item &it = items[i];
-      if ((st = npr_dev_parse_extract(c, it.input, it.len, it.start, (npr_endianness)it.endianness, &it.out, stream)))
-        return st;
-      ++i;
-    }
+  for (uint32_t i = 0; i < n; ++i) {
+    const npr_batch_item &it = items[i];
+    if (npr_status st = npr_dev_parse_extract(c, it.input, it.len, it.start, (npr_endianness)it.endianness, &it.out, stream))
+      return st;
   }
   return NPR_OK;
 }
@@ -1508,6 +1471,7 @@ npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const np
     uint64_t ro = 0, oo = 0;
     const uint64_t fo = 0, vo = a16(n * sizeof(npr_flow)), so = vo + a16(n * sizeof(npr_flow_v6));
     if ((st = small_arena(c, in, len, records, n, so + n, ar, ro, oo))) return st;
+    if (flows_v6) memset(ar + oo + vo, 0, n * sizeof(npr_flow_v6));  // the kernel writes IPv6 flows' side rows only
     HIP_CHECK(c, npr::launch_extract_dense(ar, len, (const npr_record *)(ar + ro), n, (uint32_t *)(ar + oo + fo),
                                            (uint32_t *)(ar + oo + vo), ar + oo + so, c->stream));
     HIP_CHECK(c, hipStreamSynchronize(c->stream));
@@ -1524,9 +1488,11 @@ npr_status npr_extract_flows(npr_ctx *c, const uint8_t *in, size_t len, const np
   if ((st = ensure(c, c->flows_v6, n * sizeof(npr_flow_v6)))) return st;
   if ((st = ensure(c, c->status, n))) return st;
   HIP_CHECK(c, hipMemcpyAsync(c->recs.p, records, n * sizeof(npr_record), hipMemcpyHostToDevice, c->stream));
+  // the host call's side table is dense (zero rows for non-IPv6 records): the kernel writes IPv6 flows' rows only
+  if (flows_v6) HIP_CHECK(c, hipMemsetAsync(c->flows_v6.p, 0, n * sizeof(npr_flow_v6), c->stream));
   HIP_CHECK(c, npr::launch_extract_dense((const uint8_t *)c->in.p, len, (const npr_record *)c->recs.p, n,
-                                         (uint32_t *)c->flows.p, (uint32_t *)c->flows_v6.p, (uint8_t *)c->status.p,
-                                         c->stream));
+                                         (uint32_t *)c->flows.p, flows_v6 ? (uint32_t *)c->flows_v6.p : nullptr,
+                                         (uint8_t *)c->status.p, c->stream));
   if (flows) HIP_CHECK(c, hipMemcpyAsync(flows, c->flows.p, n * sizeof(npr_flow), hipMemcpyDeviceToHost, c->stream));
   if (flows_v6)
     HIP_CHECK(c, hipMemcpyAsync(flows_v6, c->flows_v6.p, n * sizeof(npr_flow_v6), hipMemcpyDeviceToHost, c->stream));

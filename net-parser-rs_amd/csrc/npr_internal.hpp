@@ -132,14 +132,6 @@ struct ParseParams {
 // k_count_tiles then k_emit_tiles, one one-wave workgroup per tile each; or (p.nwaves != 0)
 // k_parse_resident, one launch of p.nwaves persistent waves in 16-wave workgroups.
 hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s);
-// k_parse_batch: bp.n independent flows-only captures (each p[k] a resident launch's parameters,
-// its own slot region and summary, one shared epoch) in one launch of max nwaves waves
-constexpr uint32_t kMaxBatch = 8;
-struct BatchParams {
-  uint32_t n;
-  ParseParams p[kMaxBatch];
-};
-hipError_t launch_parse_batch(const BatchParams &bp, hipStream_t s);
 // resident waves per CU the hardware admits for k_parse_resident (occupancy query)
 int resident_waves_per_cu();
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,

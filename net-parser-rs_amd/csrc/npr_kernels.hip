@@ -23,9 +23,7 @@
 //     exact state before each tile from the folds and writes every record row and flow;
 //   k_parse_resident (flows-only launches, the default): persistent waves, each owning a
 //     contiguous tile range, flows kept in registers; one pass with a decoupled look-back over
-//     16-wave workgroup aggregates (chained launches for captures past what registers hold);
-//   k_parse_batch: several independent captures in one resident launch, each capture's look-back
-//     and row writes overlapping the read of the next one's first tiles.
+//     16-wave workgroup aggregates (chained launches for captures past what registers hold).
 // A wrong speculation costs a wait or a re-walk, never a wrong result.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -1254,7 +1252,7 @@ template <uint32_t N>
 __device__ __forceinline__ uint32_t stg_slot(uint32_t c) { return (c & 1u) ? N / 2u + 8u + (c >> 1) : c >> 1; }
 
 constexpr int kPolSc1 = 16;  // buffer-store cache policy: sc1 (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16)
-// 16-B flow-row store, one row per lane (the batched pass, IPv6 side rows).  Plain (write-back):
+// 16-B flow-row store, one row per lane (IPv6 side rows, res_emit's re-read rows).  Plain (write-back):
 // measured 33.9 us per launch against 38.1 us with write-through (sc1) stores in round 1's kernel,
 // which stored every row this way (phase B's row blocks are written through since round 3).
 __device__ __forceinline__ void st_wt16(uint32_t *p, u32x4 v) { *reinterpret_cast<u32x4 *>(p) = v; }
@@ -1348,59 +1346,17 @@ struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS 
   uint32_t fail;   // a bounded wait of wave 0 timed out: every wave leaves
 };
 
-// What staging a capture's first tiles needs of its parameters (res_stage), passed by value: the
-// batch kernel reads them from its kernel arguments as scalars.
-struct StageParams {
-  const uint8_t *buf;
-  uint64_t len, org, ref;
-  uint32_t ntiles, nwaves, flags;
-};
-__device__ __forceinline__ StageParams stage_params(const ParseParams &kp) {
-  return StageParams{kp.buf, kp.len, kp.org, kp.ref, kp.ntiles, kp.nwaves, kp.flags};
-}
-
-// The first n tiles of wave v's range in a capture into its LDS ring (slots 0..n-1), behind the
-// capture's speculation-context bytes (issued first, so they land with the first tile).  Returns
-// those bytes (spec_ctx_load's).
-__device__ __forceinline__ uint32_t res_stage(const StageParams &q, ResShared &w, uint32_t v, uint32_t n) {
-  ParseParams kp{};  // the fields dma_tile / spec_ctx_load / res_range read
-  kp.buf = q.buf;
-  kp.len = q.len;
-  kp.org = q.org;
-  kp.ref = q.ref;
-  kp.ntiles = q.ntiles;
-  kp.nwaves = q.nwaves;
-  kp.flags = q.flags;
-  uint32_t c0 = 0, c1 = 0;
-  if (v < kp.nwaves) res_range(kp, v, c0, c1);
-  const uint32_t scb = spec_ctx_load(kp);
-  const uint64_t base = kp.org + (uint64_t)c0 * kTile;
-#pragma unroll
-  for (int k = 0; k < kResRing; ++k)
-    if ((uint32_t)k < n && c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, w.data[k]);
-  return scb;
-}
-
 // One capture of the resident pass (the kernel comment above).  Run by every wave of the workgroup.
-//   BATCH (k_parse_batch): one capture of several in the launch.  nx is the following capture
-//   (kn == bp->n: none): while this workgroup's prefix is being resolved, each wave stages the first
-//   kResRing tiles of its range of the next capture in its idle ring (the read that the look-back and the
-//   row writes would otherwise leave HBM without), so `next` starts with them landed; `staged`
-//   says this capture's tiles were staged that way, with its speculation bytes in scb.  The rows
-//   go out in 32-row blocks staged in the wave's record-offset scratch (the ring slot the
-//   single-capture pass stages row blocks in holds the next capture).
 // Returns false when the workgroup must leave the kernel (a bounded wait timed out).
-template <bool DIAG, bool PACK, bool BATCH>
-__device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &sh, bool has_next, StageParams nx,
-                                            bool staged, uint32_t &scb) {
+// (Round 3's k_parse_batch ran several captures through this body in one launch, staging capture
+// k+1's first tiles during capture k's look-back: 1.01-1.09x on 8 captures of 16 K-1 M records,
+// profiles/r04_batch_small.jsonl, under the 1.3x that would have paid for a second instantiation.)
+template <bool DIAG, bool PACK>
+__device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &sh) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar LDS bases
   const uint32_t b = blockIdx.x, v = b * kResWg + wid;
   const uint32_t nb = (kp.nwaves + kResWg - 1) / kResWg;
-  if (BATCH && b >= nb) {  // no range of this capture here (a smaller capture): stage the next one
-    if (has_next) scb = res_stage(nx, sh.w[wid], v, kResRing);
-    return true;
-  }
   const uint32_t nw = kp.nwaves - b * kResWg < kResWg ? kp.nwaves - b * kResWg : kResWg;  // waves of this workgroup
   const bool active = wid < nw;
   Stamps st;
@@ -1410,12 +1366,10 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   const uint64_t base = kp.org + (uint64_t)c0 * kTile;  // kept record offsets are relative to this
   const bool spec0 = (kp.flags & kFlagSpecStart) != 0 || kp.prev != nullptr;  // chained: tile 0 speculates too
   if (lane == 0) sh.prog[wid] = active && c0 < c1 ? 0u : ~0u;
-  if (!staged) {
-    scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
+  const uint32_t scb = spec_ctx_load(kp);  // older than the ring's DMAs: landed with the first tile
 #pragma unroll
-    for (int k = 0; k < kResRing - 1; ++k)
-      if (c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
-  }
+  for (int k = 0; k < kResRing - 1; ++k)
+    if (c0 + k < c1) dma_tile<2>(kp, base + (uint64_t)k * kTile, sh.w[wid].data[k]);
   __builtin_amdgcn_s_setprio(3);  // lowered by one per tile parsed (below)
 
   // ---- phase A ------------------------------------------------------------------------------
@@ -1437,16 +1391,10 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
     const uint32_t k = t - c0, slot = k % kResRing;
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    // (staged: tiles 0 .. kResRing-1 are already in flight)
-    if (t + kResRing - 1 < c1 && (!staged || k >= 1u))
+    if (t + kResRing - 1 < c1)
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
     const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (staged && k == 0u) {  // the staged tiles and the previous capture's row stores: all of them
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      wave_sync();
-    } else {
-      res_wait<0>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
-    }
+    res_wait<0>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
     if (DIAG) wait_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
     if (t == c0) {
       sc = spec_ctx(kp, scb);
@@ -1569,8 +1517,6 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  // waves 2..15 stage the next capture's first tiles now (0 and 1 hold wave 0's kept flows below)
-  if (has_next && wid >= 2u) scb = res_stage(nx, sh.w[wid], v, kResRing);
   if (wid == 0) {
     // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
     // flows wait there, so the windows get the registers.
@@ -1674,8 +1620,6 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   }
   __syncthreads();
   if (sh.fail) return false;
-  // waves 0 and 1: their rings are free again
-  if (has_next && wid < 2u) scb = res_stage(nx, sh.w[wid], v, kResRing);
   if (!active) return true;
 
   // ---- phase B ------------------------------------------------------------------------------
@@ -1685,17 +1629,6 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1 - 1);
   uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
   const bool before_end = X.exit < tile_end(kp, X.last);  // the chain ended before this range
-  // the ring re-read paths (deferred tiles, a mis-speculated range) need the ring: the staged tiles
-  // of `next` land first and are staged again afterwards
-  auto ring_take = [&]() {
-    if (has_next) {
-      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      wave_sync();
-    }
-  };
-  auto ring_give = [&]() {
-    if (has_next) scb = res_stage(nx, sh.w[wid], v, kResRing);
-  };
   if (!before_end && xe < range_hi && xe >= range_lo) {
     if (entry != kNone && xe == entry) {  // the speculated chain is the exact one: flows from registers
       if (kp.flows) {
@@ -1711,36 +1644,9 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
             // write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane
             // rounds (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s;
             // in this kernel C2 went 31.3 -> 30.8 us, and non-temporal stores a further 30.6 -> 30.1.
-            // (BATCH: the ring holds the next capture's tiles: 32-row halves through srec, below.)
             const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
             const uint64_t f0 = xo + okb;
-            if (BATCH && nok && f0 + nok <= kp.flow_cap) {
-              // the ring holds the next capture's tiles: the block goes out 32 rows at a time, staged
-              // in this wave's record-offset scratch (1 KiB, dead until the next walk; chunk c at slot
-              // c: the row stores are 2-way bank-conflicted, which the ring's stg_slot layout avoids)
-              const bool mine = (bal >> lane) & 1ull;
-              const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-              const uint64_t p = base + fl[q][7];
-              const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-              const uint32_t k = nok - 1u - rank;
-              u32x4 *stg = reinterpret_cast<u32x4 *>(sh.w[wid].srec);
-              static_assert(sizeof(sh.w[0].srec) >= 64 * 16, "32 rows fit the record-offset scratch");
-              u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
-              for (uint32_t h = 0; h < nok; h += 32u) {
-                if (mine && k >= h && k < h + 32u) {
-                  stg[2u * (k - h)] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
-                  stg[2u * (k - h) + 1u] =
-                      u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
-                }
-                wave_sync();
-                const uint32_t nh = nok - h < 32u ? nok - h : 32u;
-                const __amdgpu_buffer_rsrc_t rr =
-                    __builtin_amdgcn_make_buffer_rsrc((void *)(dst + 2u * h), 0, (int)(2u * nh * 16u), 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b128(stg[lane], rr, (int)(lane * 16u), 0, kPolSc1);
-                wave_sync();  // the scratch is rewritten by the next half
-              }
-              if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
-            } else if (!BATCH && nok && f0 + nok <= kp.flow_cap) {
+            if (nok && f0 + nok <= kp.flow_cap) {
               const bool mine = (bal >> lane) & 1ull;
               const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
               const uint64_t p = base + fl[q][7];
@@ -1773,18 +1679,14 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
       if (DIAG) stamp_at(st, 5);
       if (tdef < c1) {
         uint64_t dc = xc + cdef, dok = xo + odef;
-        ring_take();
         (void)res_emit(kp, sh.w[wid], tdef, c1, pdef, dc, dok);
-        ring_give();
         if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - tdef);
       }
       xe = pos;
       xc += cnt;
       xo += okc;
     } else {  // mis-speculated: re-read the whole range from the exact position
-      ring_take();
       xe = uni64(res_emit(kp, sh.w[wid], c0, c1, xe, xc, xo));
-      ring_give();
       if (kp.stats && lane == 0) atomicAdd(kp.stats + kStatRewalk, c1 - c0);
     }
   }
@@ -1821,28 +1723,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
 template <bool DIAG, bool PACK>
 __global__ __launch_bounds__(kResWg * kWave) void k_parse_resident(ParseParams kp) {
   __shared__ __attribute__((aligned(16))) ResWgShared sh;
-  uint32_t scb = 0;
-  (void)res_capture<DIAG, PACK, false>(kp, sh, false, StageParams{}, false, scb);
-}
-
-// =============================================================================================
-// BATCHED RESIDENT PASS — k_parse_batch: bp.n independent captures (each one resident launch's
-// worth, flows-only) in ONE launch.  The workgroups run the captures in order; capture k's
-// look-back and row writes overlap the read of capture k+1's first tiles (res_capture BATCH), and
-// the launch's own ramp and tail are paid once for the batch.  Every capture has its own slot
-// region and summary; all share the launch's epoch (so one abort stops them all).  A workgroup
-// only ever waits for LOWER workgroups of the same capture, which never wait for it: workgroups
-// drifting apart across captures cannot deadlock.
-// =============================================================================================
-template <bool PACK>
-__global__ __launch_bounds__(kResWg * kWave) void k_parse_batch(BatchParams bp) {
-  __shared__ __attribute__((aligned(16))) ResWgShared sh;
-  uint32_t scb = 0;
-  for (uint32_t k = 0; k < bp.n; ++k) {
-    const bool has_next = k + 1 < bp.n;
-    const StageParams nx = has_next ? stage_params(bp.p[k + 1]) : StageParams{};
-    if (!res_capture<false, PACK, true>(bp.p[k], sh, has_next, nx, k > 0, scb)) return;
-  }
+  (void)res_capture<DIAG, PACK>(kp, sh);
 }
 
 int resident_waves_per_cu() {
@@ -1872,15 +1753,6 @@ hipError_t launch_parse_extract(const ParseParams &p, hipStream_t s) {
     return hipGetLastError();
   }
   return (p.stats || p.stamps) ? launch<true>(p, s) : launch<false>(p, s);
-}
-
-hipError_t launch_parse_batch(const BatchParams &bp, hipStream_t s) {
-  uint32_t waves = 0;
-  for (uint32_t k = 0; k < bp.n; ++k) waves = bp.p[k].nwaves > waves ? bp.p[k].nwaves : waves;
-  if (bp.n == 0 || bp.n > kMaxBatch || waves == 0) return hipErrorInvalidValue;
-  const uint32_t nb = (waves + kResWg - 1) / kResWg;
-  hipLaunchKernelGGL(k_parse_batch<false>, dim3(nb), dim3(kResWg * kWave), 0, s, bp);
-  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2007,35 +1879,39 @@ __global__ __launch_bounds__(kBlock) void k_extract_dense(const uint8_t *buf, ui
   const uint64_t b0 = (uint64_t)blockIdx.x * kBlock, i = b0 + threadIdx.x;
   const bool act = i < n;
   uint4 r0{}, r1{}, s0{}, s1{};
+  bool is6 = false;
   if (act) {
     const npr_record rc = load_record(recs, i);
     FlowWords f{};
     const uint32_t st = extract_one(buf, len, rc, rows + threadIdx.x * kRowWords, f);
     const bool ok = st == NPR_FLOW_OK;
-    const bool is6 = ok && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16));
+    is6 = ok && (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16));
     flow_rows(f, rc.offset, ok, is6, r0, r1, s0, s1);
     if (status) status[i] = (uint8_t)st;
+  }
+  // IPv6 side rows of IPv6 flows only (npr.h): an IPv4 record's side row is not written, so an
+  // all-IPv4 batch writes 32 B per record, not 64 (C2: 32 MB of zero side rows before round 4)
+  if (is6 && flows_v6) {
+    uint4 *d6 = reinterpret_cast<uint4 *>(flows_v6 + i * 8);
+    d6[0] = s0;
+    d6[1] = s1;
   }
   // The block's rows are contiguous: stage them in LDS (the windows are done) and store whole
   // lines, 16-B chunk c by thread c % kBlock (one 32-B row per lane at a 32-B stride writes at a
   // fraction of the rate: scripts/microbench/store_pattern.hip)
+  if (!flows) return;  // (uniform)
   const uint32_t nch = 2u * (uint32_t)(n - b0 < (uint64_t)kBlock ? n - b0 : (uint64_t)kBlock);
   uint4 *stg = reinterpret_cast<uint4 *>(rows);
-  for (int t = 0; t < 2; ++t) {
-    uint32_t *out = t == 0 ? flows : flows_v6;
-    if (!out) continue;  // (uniform)
-    __syncthreads();
-    stg[stg_slot<2 * kBlock>(2 * threadIdx.x)] = t == 0 ? r0 : s0;
-    stg[stg_slot<2 * kBlock>(2 * threadIdx.x + 1)] = t == 0 ? r1 : s1;
-    __syncthreads();
-    // non-temporal (streaming) stores: 23.9 -> 23.4 us per 1M C2 records.  Write-through (sc1, or
-    // sc0 sc1), which phase B's row blocks use since round 3, measured the same here: 23.3-23.9 us
-    // for all three policies (profiles/r03_block_store_policy_ab.json)
-    uint4 *dst = reinterpret_cast<uint4 *>(out + b0 * 8);
-    if (threadIdx.x < nch) st_nt16(dst + threadIdx.x, stg + stg_slot<2 * kBlock>(threadIdx.x));
-    if (threadIdx.x + kBlock < nch)
-      st_nt16(dst + threadIdx.x + kBlock, stg + stg_slot<2 * kBlock>(threadIdx.x + kBlock));
-  }
+  __syncthreads();
+  stg[stg_slot<2 * kBlock>(2 * threadIdx.x)] = r0;
+  stg[stg_slot<2 * kBlock>(2 * threadIdx.x + 1)] = r1;
+  __syncthreads();
+  // non-temporal (streaming) stores: 23.9 -> 23.4 us per 1M C2 records.  Write-through (sc1, or
+  // sc0 sc1), which phase B's row blocks use since round 3, measured the same here: 23.3-23.9 us
+  // for all three policies (profiles/r03_block_store_policy_ab.json)
+  uint4 *dst = reinterpret_cast<uint4 *>(flows + b0 * 8);
+  if (threadIdx.x < nch) st_nt16(dst + threadIdx.x, stg + stg_slot<2 * kBlock>(threadIdx.x));
+  if (threadIdx.x + kBlock < nch) st_nt16(dst + threadIdx.x + kBlock, stg + stg_slot<2 * kBlock>(threadIdx.x + kBlock));
 }
 
 hipError_t launch_extract_dense(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,

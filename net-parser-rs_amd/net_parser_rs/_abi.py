@@ -44,7 +44,7 @@ VXLAN_PORT_IANA = 4789
 OPT_PIPE = 4  # npr_ctx_set_option: the pipelined pass (an experiment) is not built: only 0 is accepted
 OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's device window in chunks (0 auto, >= 3)
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
-PASS_TWO_PASS, PASS_RESIDENT, PASS_BATCH, PASS_SPARSE = 1, 2, 4, 8  # npr_ctx_last_pass
+PASS_TWO_PASS, PASS_RESIDENT, PASS_SPARSE = 1, 2, 8  # npr_ctx_last_pass (4, the removed batched launch, no longer occurs)
 OPT_SPARSE = 6      # npr_ctx_set_option: the sparse record walk (0 auto, 1 never, 2 always, N >= 64 lane bytes)
 OPT_SPARSE_CAP = 7  # npr_ctx_set_option: Ok-flow slots per sparse lane (0 = default 64)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
@@ -116,6 +116,7 @@ EXPORTED = [
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
     "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch", "npr_shm_all_gather",
+    "npr_stream_release",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -176,6 +177,7 @@ _SIGNATURES = {
     "npr_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_size_t, _vp, ctypes.c_size_t, _vp, _vp]),
     "npr_dev_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "npr_dev_parse_extract_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
+    "npr_stream_release": (ctypes.c_int, [_vp, _vp]),
     "npr_shm_all_gather": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
 }

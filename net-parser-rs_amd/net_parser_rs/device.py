@@ -132,9 +132,9 @@ class Workspace:
 
 
 def launch_batch(items, ctx=None, stream=None):
-    """npr_dev_parse_extract_batch: several captures in ONE resident launch.  items: (ws, buf, start,
-    endianness) per capture, each parsed as ws.launch(buf, start, endianness) would (its outputs in
-    that Workspace; check each with ws.check()).  Asynchronous on `stream` (default: the current
+    """npr_dev_parse_extract_batch: several captures in one call (one ordinary launch each, in
+    order).  items: (ws, buf, start, endianness) per capture, each parsed as ws.launch(buf, start,
+    endianness) would (its outputs in that Workspace; check each with ws.check()).  Asynchronous on `stream` (default: the current
     stream of the first buffer's device)."""
     items = list(items)
     if not items:

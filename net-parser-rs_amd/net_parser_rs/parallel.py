@@ -225,12 +225,17 @@ def gather_flows(mine: ShardResult, metas: List[ShardResult], live, group=None, 
     empty = torch.zeros(0, dtype=torch.uint8)
     fl = _as_bytes_tensor(mine.flows) if ok else empty
     # every rank must agree on whether a side table moves (a rank with no rows still takes part:
-    # the root posts one receive per contributing rank's side rows): side rows move only when every
-    # rank holds a side table, decided by one all-reduce of the flag
-    flag = torch.tensor([1 if mine.flows_v6 is not None else 0], dtype=torch.int64)
-    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
-    with_v6 = bool(flag.item())
-    v6 = (_as_bytes_tensor(mine.flows_v6) if ok else empty) if with_v6 else None
+    # the root posts one receive per contributing rank's side rows).  One MAX all-reduce of
+    # [holds a side table, has flows but no side table]: side rows move when any rank holds them; a
+    # rank without flows counts as an empty side table; a rank with flows but none while another has
+    # them would drop IPv6 addresses from the merged table, so every rank raises
+    have = mine.flows_v6 is not None
+    flag = torch.tensor([1 if have else 0, 1 if (ok and not have) else 0], dtype=torch.int64)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    with_v6, missing = bool(flag[0].item()), bool(flag[1].item())
+    if with_v6 and missing:
+        raise ValueError("gather_flows: a rank with flows has no IPv6 side table while others have one")
+    v6 = (_as_bytes_tensor(mine.flows_v6) if (ok and have) else empty) if with_v6 else None
     out, out6 = gather_flow_tables(fl, v6, metas, live, group=group, dst=dst)
     if out is None:
         return None

@@ -15,6 +15,7 @@ use crate::{check, to_record, with_ctx, PcapRecord};
 use device::Device;
 use errors::Error;
 use std::borrow::Cow;
+use std::mem::MaybeUninit;
 use std::net::{IpAddr, Ipv4Addr, Ipv6Addr};
 
 ///
@@ -55,12 +56,21 @@ impl std::fmt::Display for Flow {
 /// host->device->host round trip: for many records use [`extract_flows`] / [`convert_records`],
 /// which take the whole batch in one device call.
 ///
+/// A device failure (no usable GPU, a lost HIP context) is not a flow error: `extract_flow` and
+/// [`convert_records`] panic with the device's message, as the reference would on an allocation
+/// failure, rather than answer with an error payload or a flow list the reference never produces
+/// for that input.  `try_extract_flow` / [`try_convert_records`] return it instead.
 pub trait FlowExtraction {
     fn payload(&self) -> &[u8];
 
     fn extract_flow(&self) -> Result<Flow, Error> {
-        let mut v = extract_payloads(&[self.payload()], None);
-        v.pop().unwrap_or_else(|| Err(Error::Incomplete { size: 0 }))
+        self.try_extract_flow().unwrap_or_else(|e| panic!("net-parser-rs-amd: device failure: {}", e))
+    }
+
+    /// extract_flow, with a device failure as the outer error
+    fn try_extract_flow(&self) -> Result<Result<Flow, Error>, crate::Error> {
+        let mut v = extract_payloads(&[self.payload()], None)?;
+        Ok(v.pop().expect("one result per payload"))
     }
 }
 
@@ -70,36 +80,48 @@ impl<'a> FlowExtraction for PcapRecord<'a> {
     }
 }
 
-/// extract_flow for a batch of records in ONE device call (file order kept).
+/// extract_flow for a batch of records in ONE device call (file order kept).  Panics on a device
+/// failure (see [`FlowExtraction`]); [`try_extract_flows`] returns it.
 pub fn extract_flows<'b>(records: &[PcapRecord<'b>]) -> Vec<Result<Flow, Error>> {
+    try_extract_flows(records).unwrap_or_else(|e| panic!("net-parser-rs-amd: device failure: {}", e))
+}
+
+pub fn try_extract_flows<'b>(records: &[PcapRecord<'b>]) -> Result<Vec<Result<Flow, Error>>, crate::Error> {
     let payloads: Vec<&[u8]> = records.iter().map(|r| r.payload).collect();
     extract_payloads(&payloads, None)
 }
 
 ///
 /// Utility function to convert a vector of records to flows, unless an error is encountered
-/// in stream conversion (src/flow/mod.rs:101-123): Ok flows in REVERSE record order.
+/// in stream conversion (src/flow/mod.rs:101-123): Ok flows in REVERSE record order.  A device
+/// failure panics with the device's message (the reference drops only the records whose
+/// extract_flow failed: an empty list here would be a wrong answer); [`try_convert_records`]
+/// returns it.
 ///
 pub fn convert_records<'b>(records: Vec<PcapRecord<'b>>) -> Vec<(PcapRecord<'b>, Flow)> {
+    try_convert_records(records).unwrap_or_else(|e| panic!("net-parser-rs-amd: device failure: {}", e))
+}
+
+pub fn try_convert_records<'b>(records: Vec<PcapRecord<'b>>) -> Result<Vec<(PcapRecord<'b>, Flow)>, crate::Error> {
     convert(records, None)
 }
 
 /// convert_records when the records borrow from `input` (e.g. CaptureFile::parse(input)): the
 /// device reads the payloads from one staged copy of `input`, with no per-record gathering.
 pub fn convert_records_in<'b>(input: &'b [u8], records: Vec<PcapRecord<'b>>) -> Vec<(PcapRecord<'b>, Flow)> {
-    convert(records, Some(input))
+    convert(records, Some(input)).unwrap_or_else(|e| panic!("net-parser-rs-amd: device failure: {}", e))
 }
 
-fn convert<'b>(records: Vec<PcapRecord<'b>>, input: Option<&[u8]>) -> Vec<(PcapRecord<'b>, Flow)> {
+fn convert<'b>(records: Vec<PcapRecord<'b>>, input: Option<&[u8]>) -> Result<Vec<(PcapRecord<'b>, Flow)>, crate::Error> {
     let payloads: Vec<&[u8]> = records.iter().map(|r| r.payload).collect();
-    let res = flows_only(&payloads, input);
+    let res = flows_only(&payloads, input)?;
     let mut out = Vec::with_capacity(records.len());
     for (r, f) in records.into_iter().zip(res.into_iter()).rev() {
         if let Some(f) = f {
             out.push((r, f));
         }
     }
-    out
+    Ok(out)
 }
 
 /// The reference's `extract` bench step (benches/benches.rs:56-62: CaptureFile::parse then
@@ -110,9 +132,13 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
     let (_, header) = crate::GlobalHeader::parse(input)?;
     let big = header.endianness == nom::Endianness::Big;
     let (rows, rows6, consumed) = with_ctx(|ctx| {
+        // Capacity for the most flows the input can hold (one per 16-B record), NOT zero-filled: the
+        // device writes the n rows right-aligned, so only the pages of the last n rows are ever
+        // touched (the rest of the reservation stays virtual), and those n rows are moved into
+        // exactly sized vectors.  (Round 3 zero-filled both: 4x the input, 40 GB for a 10 GB capture.)
         let cap = input.len().saturating_sub(24) / 16 + 1;
-        let mut rows = vec![ffi::npr_flow::default(); cap];
-        let mut rows6 = vec![ffi::npr_flow_v6::default(); cap];
+        let mut rows: Vec<MaybeUninit<ffi::npr_flow>> = Vec::with_capacity(cap);
+        let mut rows6: Vec<MaybeUninit<ffi::npr_flow_v6>> = Vec::with_capacity(cap);
         let mut hdr = ffi::npr_global_header::default();
         let (mut n, mut consumed) = (0usize, 0usize);
         let st = unsafe {
@@ -121,8 +147,8 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
                 input.as_ptr(),
                 input.len(),
                 &mut hdr,
-                rows.as_mut_ptr(),
-                rows6.as_mut_ptr(),
+                rows.as_mut_ptr() as *mut ffi::npr_flow,
+                rows6.as_mut_ptr() as *mut ffi::npr_flow_v6,
                 cap,
                 &mut n,
                 &mut consumed,
@@ -131,10 +157,20 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
         };
         check(ctx, st)?;
         let k = n.min(cap);
-        // right-aligned: rows[cap - n .. cap] in convert_records order
-        rows.drain(..cap - k);
-        rows6.drain(..cap - k);
-        Ok((rows, rows6, consumed))
+        // right-aligned: rows[cap - k .. cap] in convert_records order (a side row only where the
+        // flow is IPv6: the others are taken as zero)
+        let tail: Vec<ffi::npr_flow> = (cap - k..cap).map(|i| unsafe { rows.as_ptr().add(i).read().assume_init() }).collect();
+        let tail6: Vec<ffi::npr_flow_v6> = (cap - k..cap)
+            .zip(tail.iter())
+            .map(|(i, f)| {
+                if f.kind & ffi::NPR_FLOW_KIND_IPV6 != 0 {
+                    unsafe { rows6.as_ptr().add(i).read().assume_init() }
+                } else {
+                    ffi::npr_flow_v6::default()
+                }
+            })
+            .collect();
+        Ok((tail, tail6, consumed))
     })?;
     let rd = |b: &[u8]| {
         let a = [b[0], b[1], b[2], b[3]];
@@ -188,7 +224,7 @@ pub fn vxlan_flows<'b>(
     let mut flows6 = vec![ffi::npr_flow_v6::default(); n];
     let mut status = vec![0u8; n];
     let mut vni = vec![0u32; n];
-    let r = with_ctx(|ctx| {
+    with_ctx(|ctx| {
         let st = unsafe {
             ffi::npr_vxlan_flows(
                 ctx,
@@ -205,11 +241,8 @@ pub fn vxlan_flows<'b>(
             )
         };
         check(ctx, st)
-    });
-    if let Err(e) = r {
-        let msg = format!("{}", e);
-        return (0..n).map(|_| (Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() })), 0)).collect();
-    }
+    })
+    .unwrap_or_else(|e| panic!("net-parser-rs-amd: device failure: {}", e));
     let outer = details(&payloads, input, &status);
     (0..n)
         .map(|i| {
@@ -223,9 +256,9 @@ pub fn vxlan_flows<'b>(
                 s if s > ffi::NPR_VXLAN_INNER => match s - ffi::NPR_VXLAN_INNER {
                     1 => Err(vxlan_eth_error(crate::Error::Incomplete { size: None })),
                     2 => Err(vxlan_eth_error(crate::Error::Failure { msg: String::new() })),
-                    k => Err(flow_error(k, 0, &[])),
+                    k => Err(flow_error(k, None, &[])),
                 },
-                s => Err(flow_error(s, outer[i], payloads[i])),
+                s => Err(flow_error(s, outer.as_ref().map(|d| d[i]), payloads[i])),
             };
             (res, vni[i])
         })
@@ -309,13 +342,14 @@ fn extract_raw(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<(Vec<Option<F
 }
 
 /// The error payloads (npr_flow_details) of the payloads whose status is not Ok: one more device
-/// call over those records only (0 where none was computed).
-fn details(payloads: &[&[u8]], input: Option<&[u8]>, status: &[u8]) -> Vec<u64> {
+/// call over those records only.  None when that call failed: the errors then carry no payload
+/// (size None, an explicit message) instead of a zero one.
+fn details(payloads: &[&[u8]], input: Option<&[u8]>, status: &[u8]) -> Option<Vec<u64>> {
     let n = payloads.len();
     let mut det = vec![0u64; n];
     let bad: Vec<usize> = (0..n).filter(|&i| status[i] != 0 && status[i] < ffi::NPR_VXLAN_NOT_UDP).collect();
     if bad.is_empty() {
-        return det;
+        return Some(det);
     }
     let sub: Vec<&[u8]> = bad.iter().map(|&i| payloads[i]).collect();
     let (buf, recs) = stage(&sub, input);
@@ -334,47 +368,38 @@ fn details(payloads: &[&[u8]], input: Option<&[u8]>, status: &[u8]) -> Vec<u64> 
         };
         check(ctx, st)
     });
-    if r.is_ok() {
-        for (k, &i) in bad.iter().enumerate() {
-            det[i] = got[k];
-        }
+    r.ok()?;
+    for (k, &i) in bad.iter().enumerate() {
+        det[i] = got[k];
     }
-    det
+    Some(det)
 }
 
-fn flows_only(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Option<Flow>> {
+/// Per payload Some(flow) or None; a device failure is the error (never "no flows").
+fn flows_only(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<Vec<Option<Flow>>, crate::Error> {
     if payloads.is_empty() {
-        return Vec::new();
+        return Ok(Vec::new());
     }
-    match extract_raw(payloads, input) {
-        Ok((f, _)) => f,
-        Err(_) => vec![None; payloads.len()],
-    }
+    extract_raw(payloads, input).map(|(f, _)| f)
 }
 
 /// extract_flow over `payloads` (read from `input` when they lie inside it): one device call, plus
 /// one for the error payloads of the records that failed.
-fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Vec<Result<Flow, Error>> {
+fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<Vec<Result<Flow, Error>>, crate::Error> {
     let n = payloads.len();
     if n == 0 {
-        return Vec::new();
+        return Ok(Vec::new());
     }
-    let (flows, status) = match extract_raw(payloads, input) {
-        Ok(v) => v,
-        Err(e) => {
-            let msg = format!("{}", e);
-            return (0..n).map(|_| Err(Error::NetParser(crate::Error::Custom { msg: msg.clone() }))).collect();
-        }
-    };
+    let (flows, status) = extract_raw(payloads, input)?;
     let det = details(payloads, input, &status);
-    flows
+    Ok(flows
         .into_iter()
         .enumerate()
         .map(|(i, f)| match f {
             Some(f) => Ok(f),
-            None => Err(flow_error(status[i], det[i], payloads[i])),
+            None => Err(flow_error(status[i], det.as_ref().map(|d| d[i]), payloads[i])),
         })
-        .collect()
+        .collect())
 }
 
 /// Flow::new (src/flow/mod.rs:64-86) from a 32-byte device row (+ its IPv6 side row).
@@ -405,14 +430,19 @@ fn nom_failure(p: &[u8], det: u64, kind: nom::ErrorKind<u32>) -> crate::Error {
     crate::Error::Failure { msg: format!("Error: {:?}", nom::Context::Code(input, kind)) }
 }
 
-fn flow_error(st: u8, det: u64, p: &[u8]) -> Error {
+/// The reference's error for status `st`; `det` its payload (npr_flow_details), None when it could
+/// not be computed: sizes become None and failure messages say so.
+fn flow_error(st: u8, det: Option<u64>, p: &[u8]) -> Error {
+    let known = det.is_some();
+    let det = det.unwrap_or(0);
     use crate::layer2::ethernet::{EthernetTypeId as E, Layer3Id as L3};
     use crate::layer3::InternetProtocolId as P;
     use layer2::ethernet::errors::Error as Eth;
     use layer3::{arp, ipv4, ipv6};
     type NP = crate::Error;
-    let inc = || NP::Incomplete { size: Some(det as usize) };
-    let opt = || nom_failure(p, det, nom::ErrorKind::MapOpt);
+    let inc = || NP::Incomplete { size: if known { Some(det as usize) } else { None } };
+    let unknown = || NP::Custom { msg: String::from("the error payload could not be computed (device call failed)") };
+    let opt = || if known { nom_failure(p, det, nom::ErrorKind::MapOpt) } else { unknown() };
     let eth = |e: Eth| -> Error {
         let l2: layer2::errors::Error = e.into();
         l2.into()
@@ -422,6 +452,10 @@ fn flow_error(st: u8, det: u64, p: &[u8]) -> Error {
     let v6 = || E::L3(L3::IPv6);
     let proto = || P::new(det as u8).unwrap_or(P::ICMP);
     let size = det as usize;
+    if !known && matches!(st, 3 | 6 | 9 | 11 | 12 | 13 | 15 | 16 | 23 | 24) {
+        // the error's fields ARE the payload: no guessed etype / version / protocol / size
+        return Error::NetParser(unknown());
+    }
     match st {
         1 => Error::NetParser(inc()),
         2 => Error::NetParser(opt()),
@@ -440,10 +474,10 @@ fn flow_error(st: u8, det: u64, p: &[u8]) -> Error {
         15 => l3e(ipv4::errors::Error::InternetProtocolId { id: proto() }.into()),
         16 => l3e(ipv6::errors::Error::InternetProtocolId { id: proto() }.into()),
         17 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: inc() }.into()),
-        18 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: nom_failure(p, det, nom::ErrorKind::MapRes) }.into()),
+        18 => l3e(ipv4::errors::Error::NetParser { l4: P::Tcp, err: if known { nom_failure(p, det, nom::ErrorKind::MapRes) } else { unknown() } }.into()),
         19 => l3e(ipv4::errors::Error::NetParser { l4: P::Udp, err: inc() }.into()),
         20 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: inc() }.into()),
-        21 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: nom_failure(p, det, nom::ErrorKind::MapRes) }.into()),
+        21 => l3e(ipv6::errors::Error::NetParser { l4: P::Tcp, err: if known { nom_failure(p, det, nom::ErrorKind::MapRes) } else { unknown() } }.into()),
         22 => l3e(ipv6::errors::Error::NetParser { l4: P::Udp, err: inc() }.into()),
         23 => l3e(ipv4::errors::Error::Incomplete { l4: P::Udp, size }.into()),
         24 => l3e(ipv6::errors::Error::Incomplete { l4: P::Udp, size }.into()),

@@ -8,9 +8,23 @@
 //! net-parser-rs = { package = "net-parser-rs-amd", path = ".../rust/net-parser-rs-amd" }
 //! ```
 //!
-//! and code written against the reference compiles unchanged.  The reference crate is neither a
-//! dependency nor linked: its public types are restated in this crate (`types.rs`, field for field,
-//! same `Display` strings) and every parse runs in libnpr.
+//! The reference crate is neither a dependency nor linked: the types on the record-parse and
+//! flow-extraction path are restated here (`types.rs`, field for field, same `Display` strings) and
+//! every parse runs in libnpr.
+//!
+//! **Surface.**  This crate is a drop-in for the capture -> records -> flows path (the table below)
+//! and nothing else.  Code that uses only those items compiles unchanged.  NOT restated, because
+//! they are off that path ("out of scope"):
+//! - the per-layer parsers and their structs: `layer2::ethernet::Ethernet::parse`
+//!   (src/layer2/ethernet.rs:204), `layer3::{Arp, IPv4, IPv6}::parse` (src/layer3/arp.rs:54,
+//!   ipv4.rs:148, ipv6.rs:87), `layer4::{Tcp, Udp, Vxlan}::parse` (src/layer4/tcp.rs:59, udp.rs:33,
+//!   vxlan.rs:31).  Their error types and ids ARE here (a flow error names them);
+//! - `FlowExtraction` for those layer structs (src/flow/layer2/ethernet.rs:39 ... layer4/vxlan.rs:32):
+//!   it is implemented for [`PcapRecord`] (src/flow/mod.rs:44), the one the record path uses.  The
+//!   VXLAN inner-frame flow is [`flow::vxlan_flows`], batched.
+//!
+//! A crate that also calls the per-layer parsers keeps the reference for them, under a second
+//! dependency name (`net-parser-rs-ref = { package = "net-parser-rs", version = "0.3" }`).
 //!
 //! | reference (src file:line)                          | here                                            |
 //! |----------------------------------------------------|-------------------------------------------------|
@@ -23,8 +37,12 @@
 //! | `flow::convert_records` (src/flow/mod.rs:101-123)  | [`flow::convert_records`]                       |
 //! | README `CaptureParser` facade (README.md:17-28)    | [`CaptureParser`]                               |
 //!
-//! Device errors (no GPU, a HIP failure) surface as `Error::Custom { msg }`: the reference's
-//! error enum (src/errors.rs:3-11) has no variant for them.
+//! Device errors (no GPU, a HIP failure): the parse functions return them as
+//! `Error::Custom { msg }` (the reference's error enum, src/errors.rs:3-11, has no variant for
+//! them).  `FlowExtraction::extract_flow`, `flow::extract_flows` and `flow::convert_records`,
+//! whose reference signatures cannot carry them (a per-record flow error would misreport the
+//! record, an empty flow list is a wrong answer), panic with the device's message; their `try_`
+//! forms return it.
 //!
 //! Threading: the reference's functions are pure and reentrant (its errors are Send + Sync,
 //! src/errors.rs:13-14).  Here every thread uses its own libnpr context (`thread_local!` below),
@@ -258,6 +276,8 @@ impl<'a> PcapRecords<'a> {
     /// chain is found and verified on the device (npr_records_parse).
     pub fn parse<'b>(input: &'b [u8], endianness: nom::Endianness) -> Result<(&'b [u8], PcapRecords<'b>), Error> {
         let (rows, consumed) = with_ctx(|ctx| {
+            // room for the most records the input can hold; not zero-filled, so only the pages of
+            // the n rows the device writes are ever touched (the rest stays a virtual reservation)
             let cap = input.len() / 16 + 1;
             let mut rows: Vec<ffi::npr_record> = Vec::with_capacity(cap);
             let (mut n, mut consumed) = (0usize, 0usize);

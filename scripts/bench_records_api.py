@@ -4,8 +4,8 @@ the host-memory npr_convert_records call (PCIe included), and the CPU oracle's c
 over the same record list.  Prints one JSON line.
 
 Algorithmic bytes per record: 24 (the npr_record row) + 64 (the frame the decode reads) read;
-written: convert 32 per Ok row (+ 32 for an IPv6 flow's side row), dense extract 32 + 32 + 1 B of
-status per record.  Usage: python scripts/bench_records_api.py [--records N] [--steps K]"""
+written: convert 32 per Ok row (+ 32 for an IPv6 flow's side row), dense extract 32 per record
+(+ 32 for an IPv6 flow's side row) + 1 B of status: 121 B per C2 record.  Usage: python scripts/bench_records_api.py [--records N] [--steps K]"""
 import argparse
 import ctypes
 import json
@@ -120,7 +120,7 @@ def main():
                               stream)
     n6 = int(((want_f["kind"] & _abi.KIND_IPV6) != 0).sum())
     cvt_bytes = n * (24 + 64) + len(want_f) * 32 + n6 * 32  # flow rows + side rows of IPv6 flows
-    ext_bytes = n * (24 + 64 + 64 + 1)
+    ext_bytes = n * (24 + 64 + 32 + 1) + n6 * 32  # side rows of IPv6 flows only (npr.h, since round 4)
     res = {
         "workload": f"C2 record list ({n} x 64-B frames), records + capture resident in HBM",
         "dev_convert_records": {"kernel_ms": round(cvt_ms, 5), "Mrecords_per_s": round(n / cvt_ms / 1e3, 1),

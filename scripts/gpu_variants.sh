@@ -7,7 +7,7 @@ TAG="$1"; shift
 for i in 1 2 3; do
   for v in base "$@"; do
     if [ "$v" = base ]; then L=""; else L="$R/net-parser-rs_amd/lib/libnpr_$v.so"; fi
-    NPR_LIB=$L timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu --batch 1 > gpurun_out/var_${TAG}_${v}_$i.json 2>> gpurun_out/var_$TAG.err || exit $?
+    NPR_LIB=$L timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu > gpurun_out/var_${TAG}_${v}_$i.json 2>> gpurun_out/var_$TAG.err || exit $?
     python -c "import json; d=json.load(open('gpurun_out/var_${TAG}_${v}_$i.json')); print('c2 $v $i', d['roofline']['kernel_ms'])"
   done
 done

@@ -13,7 +13,7 @@ for grp in \
   "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ TCC_EA0_WRREQ TCC_HIT_sum TCC_MISS_sum"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/pmc_$TAG/p$i" -o run \
-      -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu --batch 1 "$@" > "$R/gpurun_out/pmc_${TAG}_p$i.log" 2>&1
+      -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu "$@" > "$R/gpurun_out/pmc_${TAG}_p$i.log" 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -ne 0 ] && exit $rc
 done
 exit 0

@@ -175,6 +175,29 @@ static void run(npr_ctx *ctx, const char *path) {
   npr_host_free(ctx, pin);
   npr_host_free(ctx, pfl);
   npr_host_free(ctx, pfl6);
+
+  /* over-capacity outputs: NPR_ERR_CAPACITY with the exact counts, nothing written past the cap
+   * (the paths the Rust crate turns into Error::Custom; a short table is never a silent answer) */
+  if (on > 1) {
+    size_t n5 = 0, c5 = 0;
+    rec[on - 1].offset = 0xfeedull;
+    CHECK(npr_records_parse(ctx, in + 24, len - 24, (npr_endianness)h.endianness, rec, on - 1, &n5, &c5) ==
+                  NPR_ERR_CAPACITY && n5 == on && rec[on - 1].offset == 0xfeedull,
+          "%s: records_parse over capacity: n %zu of %zu", path, n5, on);
+  }
+  if (onf > 1) {
+    size_t n6 = 0, n7 = 0, n8 = 0, c7 = 0, c8 = 0;
+    memset(&fl[onf - 1], 0xab, sizeof *fl);
+    CHECK(npr_convert_records(ctx, in, len, orec, on, fl, fl6, onf - 1, &n6) == NPR_ERR_CAPACITY && n6 == onf &&
+              fl[onf - 1].vlan == 0xabab,
+          "%s: convert_records over capacity: n %zu of %zu", path, n6, onf);
+    CHECK(npr_parse_extract(ctx, in, len, &h, NULL, 0, &nr3, fl, fl6, onf - 1, &n7, &c7) == NPR_ERR_CAPACITY &&
+              n7 == onf && fl[onf - 1].vlan == 0xabab,
+          "%s: parse_extract over capacity: n %zu of %zu", path, n7, onf);
+    CHECK(npr_parse_extract_pipelined(ctx, in, len, &h, fl, fl6, onf - 1, &n8, &c8, 1u << 16) == NPR_ERR_CAPACITY &&
+              n8 == onf,
+          "%s: parse_extract_pipelined over capacity: n %zu of %zu", path, n8, onf);
+  }
   free(rec), free(fl), free(fl6), free(st), free(ost), free(dfl), free(dfl6);
   printf("%s: %zu records, %zu flows, consumed %zu of %zu\n", path, on, onf, ocons, len);
 done:
@@ -184,7 +207,10 @@ done:
 int main(int argc, char **argv) {
   CHECK(npr_abi_version() == NPR_ABI_VERSION, "ABI %d vs header %d", npr_abi_version(), NPR_ABI_VERSION);
   printf("%s\n", npr_version());
-  npr_ctx *ctx = NULL;
+  npr_ctx *ctx = NULL, *bad = (npr_ctx *)&failures;
+  /* a device that does not exist: an error and no context, never a context that answers "empty" */
+  CHECK(npr_ctx_create(4096, &bad) == NPR_ERR_DEVICE && bad == NULL, "ctx_create(4096) must fail");
+  CHECK(npr_ctx_create(0, NULL) == NPR_ERR_ARG, "ctx_create(NULL out)");
   if (npr_ctx_create(0, &ctx) != NPR_OK) {
     fprintf(stderr, "no HIP device\n");
     return 2;

@@ -1,10 +1,8 @@
-"""npr_dev_parse_extract_batch (k_parse_batch): several independent captures in ONE resident
-launch, each capture's results bit-exact against the oracle (and so equal to its own
-npr_dev_parse_extract).  Cases: full-size C2 batches (the bench's batched line), mixed corpora and
-endiannesses, the same capture bytes in several items, items a batch does not take (a record table
-requested, an empty capture, one larger than a launch holds) between batchable ones, more items than
-one launch takes (kMaxBatch = 8), and the capped-wave variant whose deferred tiles re-read through a
-ring holding the next capture's staged tiles."""
+"""npr_dev_parse_extract_batch: several independent captures in one call (each item the ordinary
+npr_dev_parse_extract launch, in order on the stream), each item's results bit-exact against the
+oracle.  Cases: mixed corpora and endiannesses, the same capture bytes in several items, an item
+asking for per-record status and an empty capture between flows-only ones, more than 8 items, and
+bare records (start 0).  (Round 3's one-launch k_parse_batch is gone: DESIGN.md §3.1a.)"""
 import numpy as np
 import pytest
 import torch
@@ -53,12 +51,6 @@ def run_batch(blobs, starts=None, endians=None, status=None):
     return items
 
 
-@pytest.mark.parametrize("k", [2, 4, 8])
-def test_full_size_c2_batches(k):
-    blobs = [synth.fixed64(1_000_000, seed=100 + i) for i in range(k)]
-    run_batch(blobs)
-
-
 def test_mixed_corpora_and_endianness():
     blobs = [synth.quirk_corpus(6_000, seed=41), synth.variable_mix(20_000),
              synth.quirk_corpus(4_000, seed=42, big=True, fake_every=5, jumbo_every=300),
@@ -86,14 +78,3 @@ def test_more_items_than_one_launch():
 def test_bare_records_items():
     body = synth.quirk_corpus(3_000, seed=49, with_header=False)
     run_batch([body, synth.fixed64(5_000, seed=51)], starts=[0, 24], endians=[npr.Endianness.Little, None])
-
-
-@pytest.mark.parametrize("waves", [7, 100])
-def test_capped_waves_deferred_tiles(waves):
-    ctx = npr.context(0)
-    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, waves))
-    try:
-        run_batch([synth.fixed64(60_000, seed=52), synth.quirk_corpus(8_000, seed=53, jumbo_every=400),
-                   synth.variable_mix(15_000)])
-    finally:
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))

@@ -88,3 +88,29 @@ def test_two_threads_own_contexts():
         t.join(240)
         assert not t.is_alive(), "a thread did not finish"
     assert not errors, errors
+
+
+def test_stream_release_before_destroy():
+    """A caller-created HIP stream used for a launch, handed over with npr_stream_release, then
+    destroyed; another context's next launch (whose order wait would have recorded the pending event
+    on the freed stream) runs and is exact."""
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = 200_000
+    blob = synth.fixed64(n, seed=9)
+    nr, cons, want, _ = expected(blob)
+    dev = torch.device("cuda", 0)
+    buf = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    a, b = (device.Workspace(n, n, records=False, status=False, ctx=npr.Context(0)) for _ in range(2))
+    torch.cuda.synchronize()
+    raw = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(raw)) == 0
+    a.launch(buf, start=24, stream=torch.cuda.ExternalStream(raw.value, device=dev))
+    sm = a.check()  # (on the launch's stream: before it is destroyed)
+    assert (sm.n_records, sm.n_flows, sm.consumed) == (nr, nr, cons) and a.flows_np().tobytes() == want
+    a.ctx.check(a.ctx.lib.npr_stream_release(a.ctx.handle, raw))
+    assert hip.hipStreamDestroy(raw) == 0
+    s = torch.cuda.Stream(dev)
+    b.launch(buf, start=24, stream=s)
+    sm = b.check()
+    assert (sm.n_records, sm.n_flows, sm.consumed) == (nr, nr, cons) and b.flows_np().tobytes() == want

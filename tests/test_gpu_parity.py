@@ -64,24 +64,6 @@ def check_flows(w, want):
     return sm
 
 
-def check_batch(blob, start=24, endianness=None):
-    """The capture as the middle item of a three-capture npr_dev_parse_extract_batch (k_parse_batch:
-    its first tiles staged during the previous capture's prefix, the next capture's staged during
-    its own), every item against the oracle."""
-    fillers = [synth.fixed64(3_000, seed=77), synth.quirk_corpus(700, seed=78, big=True)]
-    blobs = [fillers[0], blob, fillers[1]]
-    starts = [24, start, 24]
-    wants = [expect(b, s_, endianness if i == 1 else None) for i, (b, s_) in enumerate(zip(blobs, starts))]
-    items = []
-    for b, s_, want in zip(blobs, starts, wants):
-        cap = max((len(b) - s_) // 16 + 1, 1)
-        w = device.Workspace(cap, cap, records=False, status=False)
-        items.append((w, to_dev(b), s_, want[5]))
-    device.launch_batch(items)
-    sms = [check_flows(it[0], want) for it, want in zip(items, wants)]
-    return sms[1]
-
-
 def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     """Run the device path on `blob` and compare everything with the oracle.
 
@@ -90,21 +72,11 @@ def check_parity(blob, start=24, endianness=None, ws=None, light=False):
     default for flows-only launches); light=N (an int > 1) the same with at most N waves, so
     each wave owns a long tile range (kept-round overflow -> deferred tiles, many ranges per
     64-wave group, speculation at range starts deep inside the capture); light="decode" the
-    two-pass kernels (NPR_OPT_RESIDENT off); light="batch" / "batch_wN" the capture inside a batched
-    launch (k_parse_batch), the latter with at most N waves per capture (deferred tiles re-read
-    through a ring that holds the next capture's staged tiles); light="sparse" the sparse record walk
+    two-pass kernels (NPR_OPT_RESIDENT off); light="sparse" the sparse record walk
     forced (NPR_OPT_SPARSE 2), "sparse_sN" with lane ranges of N bytes, "..._cK" with K Ok-flow
     slots per lane (lanes past their slots walk the rest again when rows are written)."""
     if isinstance(light, str) and light.startswith("sparse"):
         return check_sparse(blob, start, endianness, ws, light)
-    if isinstance(light, str) and light.startswith("batch"):
-        ctx = npr.context(0)
-        cap = int(light[7:]) if light.startswith("batch_w") else 1
-        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, cap))
-        try:
-            return check_batch(blob, start, endianness)
-        finally:
-            ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 1))
     if light == "decode" or (light is not True and isinstance(light, int) and light > 1):
         ctx = npr.context(0)
         ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_RESIDENT, 0 if light == "decode" else light))
@@ -210,10 +182,10 @@ def test_kat_frames_as_records(name):
 # resident_w16 / _w48: whole 16-wave workgroups (one and three), long ranges with deferred tiles
 # sparse: the sparse record walk forced; _s256: 256-B lane ranges (records span many lanes, most
 # lanes speculate inside payloads); _s4096_c2: two Ok-flow slots per lane (the overflow walk)
-LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode", "batch", "batch_w7", "batch_w100",
+LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode",
                                           "sparse", "sparse_s256", "sparse_s4096_c2"],
                                 ids=["full", "resident", "resident_w7", "resident_w100", "resident_w16",
-                                     "resident_w48", "two_pass", "batch", "batch_w7", "batch_w100",
+                                     "resident_w48", "two_pass",
                                      "sparse", "sparse_s256", "sparse_s4096_c2"])
 
 

@@ -1,5 +1,6 @@
-"""INTEGRATION.md quotes the Rust crate (rust/net-parser-rs-amd) byte for byte, and every function
+"""INTEGRATION.md quotes the Rust crate's FFI binding byte for byte and lists its API files by hash, and every function
 the crate's FFI module binds is declared in include/npr.h and exported by libnpr.so."""
+import hashlib
 import os
 import re
 import subprocess
@@ -13,9 +14,14 @@ CRATE = os.path.join(REPO, "rust", "net-parser-rs-amd")
 def test_integration_md_quotes_the_committed_crate():
     doc = open(os.path.join(REPO, "INTEGRATION.md")).read()
     blocks = re.findall(r"### `rust/net-parser-rs-amd/([^`]+)`\n\n````[a-z]+\n(.*?)````\n", doc, re.S)
-    assert {f for f, _ in blocks} == {"Cargo.toml", "build.rs", "src/ffi.rs", "src/lib.rs", "src/types.rs", "src/flow.rs"}
+    assert {f for f, _ in blocks} == {"Cargo.toml", "build.rs", "src/ffi.rs"}
     for f, body in blocks:
         assert body == open(os.path.join(CRATE, f)).read(), f"INTEGRATION.md is stale for {f}: run scripts/gen_integration.py"
+    listed = re.findall(r"\| `rust/net-parser-rs-amd/([^`]+)` \| (\d+) \| `([0-9a-f]{16})` \|", doc)
+    assert {f for f, _, _ in listed} == {"src/lib.rs", "src/types.rs", "src/flow.rs"}
+    for f, _, h in listed:
+        got = hashlib.sha256(open(os.path.join(CRATE, f), "rb").read()).hexdigest()[:16]
+        assert got == h, f"INTEGRATION.md is stale for {f}: run scripts/gen_integration.py"
 
 
 def test_ffi_rs_binds_only_declared_and_exported_symbols():
