@@ -340,17 +340,8 @@ __device__ __forceinline__ uint64_t lane_walk(const ParseParams &kp, uint32_t *r
     uint32_t wn[kSpWords];
     if (more) load_chunks<0, 5>(align16(kp.buf + next), end, wn);
     FlowWords f{};
-#if defined(NPR_SP_EXP_HOP)  // timing experiment only: the hops, no decode, no slots
-    const uint32_t st = w[4] == 0x12345678u ? 1u : 0u;
-    asm volatile("" ::"v"(w[5]), "v"(w[19]));
-#else
     const uint32_t st = rec_decode(kp, row, pp, avail, rel, incl, w, f);
-#endif
-#if !defined(NPR_SP_EXP_HOP) && !defined(NPR_SP_EXP_NOSLOT)
     sink(pos, st == NPR_FLOW_OK, f);
-#else
-    asm volatile("" ::"v"(st), "v"(f.d[2]));
-#endif
     ++cnt;
     pos = next;
     if (!more) break;
@@ -368,28 +359,11 @@ __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 
 }
 // every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
 // wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded
-// 16-B store with a cache policy (timing variants: 0 plain write-back, 1 non-temporal, 2 write-
-// through sc1, 3 sc0 sc1)
-template <int POL>
-__device__ __forceinline__ void store16(u32x4 *d, u32x4 v) {
-  if constexpr (POL == 1) {
-    __builtin_nontemporal_store(v, d);
-  } else if constexpr (POL == 2) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(d), "v"(v) : "memory");
-  } else if constexpr (POL == 3) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(d), "v"(v) : "memory");
-  } else {
-    *d = v;
-  }
-}
-#ifndef NPR_SP_SLOT_POLICY
-#define NPR_SP_SLOT_POLICY 0
-#endif
-#ifndef NPR_SP_ROW_POLICY
-#define NPR_SP_ROW_POLICY 0
-#endif
-__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) { store16<NPR_SP_SLOT_POLICY>(d, v); }
-__device__ __forceinline__ void row_store(u32x4 *d, u32x4 v) { store16<NPR_SP_ROW_POLICY>(d, v); }
+// Slots and rows are plain (write-back) stores: non-temporal and write-through (sc1, sc0 sc1)
+// stores measured slower for both the scattered slot rows and the whole-line row blocks (DESIGN.md
+// §3.8)
+__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) { *d = v; }
+__device__ __forceinline__ void row_store(u32x4 *d, u32x4 v) { *d = v; }
 struct AreaSink {
   u32x4 *slot0;  // the lane's slot 0 (its first 16 B); NULL: count only
   uint32_t cap, n, okn;

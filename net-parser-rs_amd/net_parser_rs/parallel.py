@@ -345,10 +345,17 @@ class ShmExchange:
             raise RuntimeError(f"ShmExchange: cannot create {path}")
         try:
             self.mm = np.memmap(path, dtype=np.uint8, mode="r+", shape=(size,))
-        finally:
-            dist.barrier(group=group)  # every rank mapped (or failed): the name is no longer needed
-            if self.rank == 0:
-                os.unlink(path)
+            mapped = True
+        except (OSError, ValueError):
+            mapped = False
+        # every rank mapped (or failed): the name is no longer needed, and every rank agrees on the
+        # outcome (one rank falling back alone would leave the others in an exchange it never joins)
+        flags = [None] * self.world
+        dist.all_gather_object(flags, mapped, group=group)
+        if self.rank == 0:
+            os.unlink(path)
+        if not all(flags):
+            raise RuntimeError(f"ShmExchange: {path} could not be mapped on every rank")
         grid = self.mm.reshape(self.world, self.depth, self.rec)
         self.seqs = grid.view(np.uint64)[:, :, 0]  # [rank, slot]: the slot's sequence number
         self.pay = grid[:, :, self.HEADER:]         # [rank, slot, byte]
