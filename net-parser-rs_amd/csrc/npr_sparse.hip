@@ -929,6 +929,11 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   const uint32_t j = tid >> 2, sub = tid & 3u;
   const uint64_t mj = msk[j];
   const uint32_t pj = opre[j];
+  // the slots this thread stages are always lane (tid >> 1) & 63's (q = tid + 256 u): load a slot
+  // row's 16-B chunk only when one of the four lanes sharing its 128-B line has an Ok flow there
+  // (lanes hold ~48 records of up to 64 slots: C3's rows kernel read 313 MB for 256 MB of slots)
+  const uint32_t lq = ((tid >> 1) & 63u) & ~3u;
+  const uint64_t lmask = msk[lq] | msk[lq + 1] | msk[lq + 2] | msk[lq + 3];
   for (uint32_t k0 = 0; k0 < kmax; k0 += kRowChunk) {
     const uint32_t nk = kmax - k0 < kRowChunk ? kmax - k0 : kRowChunk;
     {  // every slot load in flight before the first LDS store
@@ -937,7 +942,8 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
 #pragma unroll
       for (uint32_t u = 0; u < kPer; ++u) {
         const uint32_t q = tid + u * kSpBlock;
-        v[u] = area[(uint64_t)k0 * 128u + (q < nk * 128u ? q : 0u)];
+        const uint32_t kk = k0 + (q >> 7);
+        v[u] = q < nk * 128u && ((lmask >> kk) & 1ull) ? area[(uint64_t)k0 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
       }
 #pragma unroll
       for (uint32_t u = 0; u < kPer; ++u) {
