@@ -179,7 +179,8 @@ constexpr uint64_t kSparseMinBytes = 256ull << 20;
 constexpr uint64_t kSparseMinMean = 384;            // ... of at least this many bytes per record (16 + incl)
 constexpr uint64_t kSparseSpanDefault = 16u << 10;  // lane range when the density is unknown
 constexpr uint64_t kSparseSpanRecords = 48;         // lane range of a small range: this many mean records (24 -> 48: C3 walk 573 -> 508 us)
-constexpr uint64_t kSparseLaneRecords = 56;         // most mean records per lane when the range fills the chip (slots: 64)
+constexpr uint64_t kSparseLaneRecords = 64;         // most mean records per lane when the range fills the chip (slots: 64;
+                                                    // C3 at 61 per lane: 0.635 ms, 2.47 GB; at 41: 0.637 ms, 2.59 GB)
 constexpr uint64_t kSparseCuLanes = 256;            // lanes of one k_sparse_walk workgroup (kSpBlock)
 // Records from the exact record start `start` in the capture's first kProbeBytes: *n and their
 // bytes per record (header included), 0 when fewer than 16 fit.  One pinned D2H copy and a sync,
@@ -235,7 +236,7 @@ npr_status sparse_choice(npr_ctx *c, const void *input, uint64_t start, uint64_t
   }
   uint64_t sized = std::min<uint64_t>(std::max<uint64_t>(kSparseSpanRecords * mean, 4u << 10), 1u << 20);
   // A range of more records than one 256-lane workgroup per CU holds at ~24 each: k workgroups per CU
-  // exactly (k = the fewest that keep lanes at <= 56 mean records).  The walk is bound per CU (its
+  // exactly (k = the fewest that keep lanes at <= 64 mean records: fewer lanes speculate less).  The walk is bound per CU (its
   // random 16-B loads), so its time follows the most lane-records any CU holds: C3 at 36.9 … 61 KB
   // lanes took 0.636–0.716 ms in step with that maximum (3 workgroups on some CUs and 2 on others:
   // 0.716; 2 or 3 on every CU: 0.636), profiles/r04_c3_span_sweep.json.

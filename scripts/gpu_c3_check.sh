@@ -8,8 +8,10 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -k "sparse"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_scale.py -x -q -k c3 --timeout 250 --timeout-method thread -p no:cacheprovider > "gpurun_out/${TAG}_c3.log" 2>&1 || exit $?
 timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 2 --no-cpu > "gpurun_out/${TAG}_bench_c3.json" 2> "gpurun_out/${TAG}_bench_c3.err" || exit $?
 cd /tmp && export TMPDIR=/tmp
+i=0
 for grp in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/pmc_${TAG}_c3/$grp" -o run \
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$R/gpurun_out/pmc_${TAG}_c3/p$i" -o run \
       -- python3 "$R/bench.py" --config c3 --steps 2 --warmup 1 --no-cpu > "$R/gpurun_out/pmc_${TAG}_c3_$grp.log" 2>&1 || exit $?
 done
 cd "$R" && python scripts/pmc_json.py "${TAG}_c3" "gpurun_out/${TAG}_pmc_c3.json" c3 || exit $?
