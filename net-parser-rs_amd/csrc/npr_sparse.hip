@@ -875,83 +875,94 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
 // k_sparse_rows: group w's Ok flows (file order i = 0 .. okw-1, global index O + i) to rows
 // flow_cap - 1 - (O + i).  The group's slots go through LDS kRowChunk slot rows at a time: read
 // as 1-KiB contiguous pieces, written back as each lane's run of consecutive rows (thread 4j + s
-// takes lane j's slots k0 + s + 4m: the four threads of a lane store neighbouring rows).
+// takes lane j's slots k0 + s + 4m: the four threads of a lane store neighbouring rows).  The next
+// chunk's loads are in flight (registers) while the current one is written; the first chunk's are
+// issued before the lanes' chain walk-through, which wave 0 runs from registers.
 // =============================================================================================
-#ifndef NPR_SP_ROW_CHUNK
-#define NPR_SP_ROW_CHUNK 16
-#endif
-constexpr uint32_t kRowChunk = NPR_SP_ROW_CHUNK;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
+constexpr uint32_t kRowChunk = 16;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
+constexpr uint32_t kRowPer = kRowChunk * 128u / kSpBlock;  // 16-B slot chunks per thread per stage
 __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   __shared__ uint32_t opre[65];
   __shared__ uint32_t okl[64], sl[64];  // Ok flows of the lane, in its slots
   __shared__ uint64_t ovf[64], hil[64], msk[64];
   __shared__ uint32_t kmax_sh;
-  __shared__ SparseLane ls[64];
   __shared__ __attribute__((aligned(16))) u32x4 stage[kRowChunk * 64 * 2];
   const ParseParams &kp = sp.kp;
   const uint32_t w = blockIdx.x, tid = threadIdx.x;
   if (__hip_atomic_load(sp.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gran(kp.epoch, 1)) return;
-  const SparsePre P = sp.pre[w];
+  const u32x4 *area = reinterpret_cast<const u32x4 *>(sp.area) + (uint64_t)w * sp.cap * 128u;
+  // the first chunk (slot rows 0 .. 15 of every lane): lanes hold ~40-60 records, so these are
+  // nearly always needed; loaded while wave 0 works out which lanes the chain runs through
+  u32x4 v[kRowPer];
+  const uint32_t n0 = sp.cap < kRowChunk ? sp.cap * 128u : kRowChunk * 128u;  // (the group's slot area: cap rows)
+#pragma unroll
+  for (uint32_t u = 0; u < kRowPer; ++u) {
+    const uint32_t q = tid + u * kSpBlock;
+    v[u] = q < n0 ? area[q] : u32x4{0u, 0u, 0u, 0u};
+  }
   const uint64_t l0 = (uint64_t)w * 64;
   const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
-  if (tid < size) ls[tid] = sp.lanes[l0 + tid];
-  __syncthreads();
-  if (tid == 0) {  // which lanes the exact chain runs through (every link is consistent now)
-    uint64_t s = P.exit;
-    bool ended = s < sp_end(sp, (int64_t)l0 - 1);
-    uint32_t acc = 0, km = 0;
-    for (uint32_t j = 0; j < 64; ++j) {
-      opre[j] = acc;
-      okl[j] = 0;
-      sl[j] = 0;
-      msk[j] = 0;
-      if (j >= size || ended) continue;
-      const uint64_t hi = sp_end(sp, (int64_t)(l0 + j));
-      if (s >= hi) continue;  // a record spans the lane
-      const SparseLane &L = ls[j];
-      okl[j] = L.ok;
-      msk[j] = L.okmask;
-      sl[j] = (uint32_t)__builtin_popcountll(L.okmask);
-      if (L.okmask) km = max(km, 64u - (uint32_t)__builtin_clzll(L.okmask));
-      ovf[j] = L.ovf;
-      hil[j] = hi;
-      acc += L.ok;
-      s = L.exit;
-      ended = s < hi;
+  if (tid < 64) {  // wave 0: lane tid's walk; which lanes the exact chain runs through (every link is consistent now)
+    const SparsePre P = sp.pre[w];
+    const bool in = tid < size;
+    SparseLane L{};
+    if (in) L = sp.lanes[l0 + tid];
+    const uint64_t hi = in ? sp_end(sp, (int64_t)(l0 + tid)) : 0ull;
+    // the serial rule, on wave-uniform values: a lane whose end the chain position has passed is
+    // spanned by a record (skipped); a lane whose exit is short of its end ends the chain
+    uint64_t pos = P.exit, part = 0;
+    bool ended = pos < sp_end(sp, (int64_t)l0 - 1);
+    for (uint32_t j = 0; j < size && !ended; ++j) {
+      const uint64_t hj = rl64(hi, (int)j);
+      if (pos >= hj) continue;
+      part |= 1ull << j;
+      pos = rl64(L.exit, (int)j);
+      ended = pos < hj;
     }
-    opre[64] = acc;
-    kmax_sh = km;
+    const bool me = (part >> tid) & 1ull;
+    const uint32_t ok = me ? L.ok : 0u;
+    const uint64_t m = me ? L.okmask : 0ull;
+    const uint32_t ex = excl_scan_u32(ok);
+    opre[tid] = ex;
+    okl[tid] = ok;
+    msk[tid] = m;
+    sl[tid] = (uint32_t)__builtin_popcountll(m);
+    ovf[tid] = L.ovf;
+    hil[tid] = hi;
+    uint32_t km = m ? 64u - (uint32_t)__builtin_clzll(m) : 0u;
+    for (int o = 32; o > 0; o >>= 1) km = max(km, (uint32_t)__shfl_xor((int)km, o));
+    if (tid == 63) opre[64] = ex + ok;
+    if (tid == 0) kmax_sh = km;
   }
   __syncthreads();
   const uint32_t kmax = kmax_sh;
-  const uint64_t O = P.ok;
-  const u32x4 *area = reinterpret_cast<const u32x4 *>(sp.area) + (uint64_t)w * sp.cap * 128u;
+  const uint64_t O = sp.pre[w].ok;
   const uint32_t j = tid >> 2, sub = tid & 3u;
   const uint64_t mj = msk[j];
   const uint32_t pj = opre[j];
-  // the slots this thread stages are always lane (tid >> 1) & 63's (q = tid + 256 u): load a slot
-  // row's 16-B chunk only when one of the four lanes sharing its 128-B line has an Ok flow there
-  // (lanes hold ~48 records of up to 64 slots: C3's rows kernel read 313 MB for 256 MB of slots)
+  // the slots this thread stages are always lane (tid >> 1) & 63's (q = tid + 256 u): a later chunk
+  // loads a slot row's 16-B chunk only when one of the four lanes sharing its 128-B line has an Ok
+  // flow there (C3's rows kernel read 313 MB for 256 MB of slots before)
   const uint32_t lq = ((tid >> 1) & 63u) & ~3u;
   const uint64_t lmask = msk[lq] | msk[lq + 1] | msk[lq + 2] | msk[lq + 3];
   for (uint32_t k0 = 0; k0 < kmax; k0 += kRowChunk) {
     const uint32_t nk = kmax - k0 < kRowChunk ? kmax - k0 : kRowChunk;
-    {  // every slot load in flight before the first LDS store
-      constexpr uint32_t kPer = kRowChunk * 128u / kSpBlock;
-      u32x4 v[kPer];
 #pragma unroll
-      for (uint32_t u = 0; u < kPer; ++u) {
-        const uint32_t q = tid + u * kSpBlock;
-        const uint32_t kk = k0 + (q >> 7);
-        v[u] = q < nk * 128u && ((lmask >> kk) & 1ull) ? area[(uint64_t)k0 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kPer; ++u) {
-        const uint32_t q = tid + u * kSpBlock;
-        if (q < nk * 128u) stage[q] = v[u];
-      }
+    for (uint32_t u = 0; u < kRowPer; ++u) {
+      const uint32_t q = tid + u * kSpBlock;
+      if (q < nk * 128u) stage[q] = v[u];
     }
     __syncthreads();
+    const uint32_t k1 = k0 + kRowChunk;
+    if (k1 < kmax) {  // the next chunk's loads, in flight while this one is written
+      const uint32_t nk1 = kmax - k1 < kRowChunk ? kmax - k1 : kRowChunk;
+#pragma unroll
+      for (uint32_t u = 0; u < kRowPer; ++u) {
+        const uint32_t q = tid + u * kSpBlock;
+        const uint32_t kk = k1 + (q >> 7);
+        v[u] = q < nk1 * 128u && ((lmask >> kk) & 1ull) ? area[(uint64_t)k1 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
 #pragma unroll
     for (uint32_t m = 0; m < kRowChunk / 4; ++m) {
       const uint32_t k = k0 + sub + 4 * m;
