@@ -12,10 +12,7 @@ namespace npr {
 // Tile geometry of the parse+extract kernels: ONE WAVE per tile.
 constexpr int kBlock = 256;            // workgroup size of the auxiliary kernels (dense extract, compaction)
 constexpr int kWave = 64;              // lanes per wave (the two-pass kernels: one-wave workgroups)
-#ifndef NPR_TILE_BYTES
-#define NPR_TILE_BYTES 4096
-#endif
-constexpr int kTile = NPR_TILE_BYTES;  // bytes of the record stream owned by one tile (one wave)
+constexpr int kTile = 4096;            // bytes of the record stream owned by one tile (one wave; 8 KiB: DESIGN.md §5)
 constexpr int kHalo = 128;             // bytes staged past the tile (headers + fast-decode window of straddlers)
 constexpr int kStage = kTile + kHalo;  // bytes staged in LDS per tile
 constexpr int kMaxRec = kTile / 16;    // every record is >= 16 B
@@ -53,18 +50,9 @@ struct alignas(128) RangeSlot {
   uint64_t pad[4];
 };
 static_assert(sizeof(RangeSlot) == sizeof(TileSlot), "range slots reuse the tile-slot allocation");
-#ifndef NPR_RES_MAX_WAVES
-#define NPR_RES_MAX_WAVES 4096
-#endif
-constexpr uint32_t kResMaxWaves = NPR_RES_MAX_WAVES;  // at most 4096 persistent waves
-#ifndef NPR_RES_SLOTS
-#define NPR_RES_SLOTS 6
-#endif
-constexpr int kResSlots = NPR_RES_SLOTS;    // 64-record rounds of flows held in registers per wave
-#ifndef NPR_RES_WG_MIN
-#define NPR_RES_WG_MIN 16
-#endif
-constexpr uint32_t kResWgMin = NPR_RES_WG_MIN;  // waves per workgroup (npr_kernels.hip kResWg) is at least this
+constexpr uint32_t kResMaxWaves = 4096;  // at most 4096 persistent waves
+constexpr int kResSlots = 6;             // 64-record rounds of flows held in registers per wave
+constexpr uint32_t kResWgMin = 16;       // waves per workgroup (npr_kernels.hip kResWg) is at least this
 
 // exclusive-prefix words: {exit, cnt, ok | valid << 32 | empty << 33, mism + 1, entry + 1}
 enum : int { kPreExit = 0, kPreCnt = 1, kPreOk = 2, kPreMism = 3, kPreEntry = 4 };

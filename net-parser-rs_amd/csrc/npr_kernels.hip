@@ -987,15 +987,9 @@ __global__ __launch_bounds__(kWave) void k_emit_tiles(ParseParams kp) {
 //     are re-read; otherwise the range is re-walked from the exact position.  A contradiction below
 //     v waits for the offending wave's exact prefix P(m), published at the end of its own phase B.
 // =============================================================================================
-#ifndef NPR_RES_RING
-#define NPR_RES_RING 2
-#endif
-constexpr int kResRing = NPR_RES_RING;    // LDS tile slots per wave (1 processed + kResRing-1 in flight)
+constexpr int kResRing = 2;               // LDS tile slots per wave (1 processed + kResRing-1 in flight)
 constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
-#ifndef NPR_RES_WG
-#define NPR_RES_WG 16
-#endif
-constexpr uint32_t kResWg = NPR_RES_WG;   // waves per workgroup (one workgroup per CU): folded in LDS
+constexpr uint32_t kResWg = 16;           // waves per workgroup (one workgroup per CU): folded in LDS
 static_assert(kResWg >= kResWgMin, "workgroup aggregate slots (npr_capi.hip group_slots) are sized for kResWgMin");
 static_assert(kResRing >= 2 && (kResRing - 1) * kDmaPer < 64, "vmcnt field is 6 bits");
 

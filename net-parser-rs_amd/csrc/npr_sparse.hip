@@ -32,9 +32,6 @@
 namespace npr {
 namespace {
 
-#ifndef NPR_SP_WAVES
-#define NPR_SP_WAVES 4
-#endif
 constexpr int kSpBlock = 256;                // walk / rows kernels: four 64-lane groups per workgroup
 constexpr int kSpWin = 112;                  // a record's full window: [header & ~15, +112) (80 B in the fast path)
 constexpr int kSpRow = kSpWin / 4 + 1;       // a lane's LDS row (odd dword stride: conflict-free)
@@ -429,7 +426,7 @@ struct RowSink {
 // =============================================================================================
 // k_sparse_walk: one lane range per lane, one 64-lane group per wave
 // =============================================================================================
-__global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(NPR_SP_WAVES))) void k_sparse_walk(SparseParams sp) {
+__global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(4))) void k_sparse_walk(SparseParams sp) {
   __shared__ uint32_t rows[kSpBlock * kSpRow];
   const ParseParams &kp = sp.kp;
   const uint32_t lane = threadIdx.x & 63u;

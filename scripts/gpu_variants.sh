@@ -1,5 +1,5 @@
 #!/bin/bash
-# Interleaved timing of in-tree library variants (make variant NAME=X ...): C2 x3 and C3 x1 each.
+# Interleaved timing of library builds of other revisions (make variant NAME=X REV=<commit>): C2 x3 and C3 x1 each.
 # Usage: gpu_variants.sh TAG X [Y ...]   (base = lib/libnpr.so)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out
