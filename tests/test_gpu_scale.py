@@ -91,6 +91,38 @@ def test_c3_full_8m_bit_exact():
     log("C3: ok")
 
 
+@pytest.mark.parametrize("big", [False, True])
+def test_adversarial_300mb_auto_sparse(big):
+    """The auto choice on a large capture of the quirk corpus (every layer's quirks, IPv6, VLANs,
+    ARP, fake header chains inside payloads, zero-length records, 20-70 KB jumbo records, a
+    truncated tail; mean record > 384 B, > 256 MiB): the sparse walk, bit-exact against the oracle
+    flows and IPv6 side rows, and against the resident pass forced."""
+    log(f"adversarial 300 MB (big={big}): generating")
+    blob = synth.quirk_corpus(360_000, seed=71 + big, big=big, jumbo_every=60, fake_every=7, zero_every=11,
+                              tail="truncated_payload")
+    assert len(blob) > (256 << 20)
+    hdr, recs, cons, flows, v6 = oracle_flows(blob)
+    n = len(recs)
+    ws = device.Workspace(record_cap=n, flow_cap=n, records=False, offsets=False, status=False,
+                          flows=True, flows_v6=True)
+    buf = to_dev(blob)
+    lib, h = ws.ctx.lib, ws.ctx.handle
+    for mode, want_pass in ((0, _abi.PASS_SPARSE), (1, _abi.PASS_RESIDENT)):
+        ws.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, mode))
+        try:
+            ws.flows.zero_()
+            ws.launch(buf, start=24, endianness=hdr.endianness)
+            sm = ws.check()
+            assert lib.npr_ctx_last_pass(h) == want_pass
+        finally:
+            ws.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, 0))
+        assert (sm.n_records, sm.n_flows, sm.consumed) == (n, len(flows), cons), mode
+        got = ws.flows_np()
+        assert got.tobytes() == flows.tobytes(), mode
+        assert v6_rows(got, ws.flows_v6_np()).tobytes() == v6_rows(flows, v6).tobytes(), mode
+    log("adversarial 300 MB: ok")
+
+
 def c4_shards(n_records, world, host=None):
     """Each rank's buffer exactly as the 8-GPU run lays it out: its own file bytes only."""
     layout = parallel.record_range_shards(n_records, world)
