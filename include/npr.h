@@ -402,7 +402,7 @@ npr_status npr_dev_parse_extract_shard(npr_ctx *ctx, const void *input, uint64_t
  * call: each item is what npr_dev_parse_extract(ctx, input, len, start, endianness, &out, stream)
  * would parse, launched in order on the stream, with the same outputs and summary (check each with
  * npr_dev_check).  (ABI 2 ran flows-only items in one batched launch; it measured 0.96-1.09x of
- * separate launches and was removed, DESIGN.md §3.1a.) */
+ * separate launches and was removed, DESIGN.md §3.2.) */
 typedef struct npr_batch_item {
   const void *input;
   uint64_t len;

@@ -1,4 +1,4 @@
-"""K small captures per k_parse_batch launch against K single resident launches.
+"""K small captures per npr_dev_parse_extract_batch call against K single launches (written for round 3's one-launch k_parse_batch, which it retired: DESIGN.md §3.2).
 
 The batched launch pays the launch ramp and tail once per K captures; it should pay where those
 dominate: many SMALL captures.  Times K x R-record C2-shaped captures (distinct buffers, 16 rounds

@@ -2,7 +2,7 @@
 npr_dev_parse_extract launch, in order on the stream), each item's results bit-exact against the
 oracle.  Cases: mixed corpora and endiannesses, the same capture bytes in several items, an item
 asking for per-record status and an empty capture between flows-only ones, more than 8 items, and
-bare records (start 0).  (Round 3's one-launch k_parse_batch is gone: DESIGN.md §3.1a.)"""
+bare records (start 0).  (Round 3's one-launch k_parse_batch is gone: DESIGN.md §3.2.)"""
 import numpy as np
 import pytest
 import torch
