@@ -185,6 +185,9 @@ def gather_flow_tables(flows, flows_v6, metas: List[ShardResult], live, group=No
     rank = dist.get_rank(group)
     pos, total = merged_positions(metas, live)
     with_v6 = flows_v6 is not None
+    if dist.get_backend(group) == "gloo":  # gloo moves host tensors only
+        flows = flows.cpu() if flows is not None else None
+        flows_v6 = flows_v6.cpu() if flows_v6 is not None else None
     gr = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
     reqs = []
     if rank != dst:
