@@ -262,8 +262,8 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   record density of the capture's first 256 KiB (at least 256 MiB past `start`, a known start, no
  *   shard); 1 never; 2 always (lane ranges sized from the density, else 16 KiB); N >= 64 always,
  *   with lane ranges of N bytes (a test knob).  Same results either way.
- * NPR_OPT_SPARSE_CAP (default 0 = 64): record slots per sparse lane; a lane with more records
- *   walks the rest again when its rows are written (a test knob; 1 .. 64).
+ * NPR_OPT_SPARSE_CAP (default 0 = 96): record slots per sparse lane; a lane with more records
+ *   walks the rest again when its rows are written (a test knob; 1 .. 128).
  */
 enum { NPR_OPT_PARK_FLOWS = 1, NPR_OPT_RESIDENT = 2, NPR_OPT_STREAM_CHUNK = 3, NPR_OPT_PIPE = 4,
        NPR_OPT_DEVICE_WINDOW = 5, NPR_OPT_SPARSE = 6, NPR_OPT_SPARSE_CAP = 7 };

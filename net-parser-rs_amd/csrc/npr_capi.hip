@@ -179,7 +179,7 @@ constexpr uint64_t kSparseMinBytes = 256ull << 20;
 constexpr uint64_t kSparseMinMean = 384;            // ... of at least this many bytes per record (16 + incl)
 constexpr uint64_t kSparseSpanDefault = 16u << 10;  // lane range when the density is unknown
 constexpr uint64_t kSparseSpanRecords = 48;         // lane range of a small range: this many mean records (24 -> 48: C3 walk 573 -> 508 us)
-constexpr uint64_t kSparseLaneRecords = 64;         // most mean records per lane when the range fills the chip (slots: 64;
+constexpr uint64_t kSparseLaneRecords = 64;         // most mean records per lane when the range fills the chip (slots: 96;
                                                     // C3 at 61 per lane: 0.635 ms, 2.47 GB; at 41: 0.637 ms, 2.59 GB)
 constexpr uint64_t kSparseCuLanes = 256;            // lanes of one k_sparse_walk workgroup (kSpBlock)
 // Records from the exact record start `start` in the capture's first kProbeBytes: *n and their
@@ -455,7 +455,7 @@ npr_status npr_ctx_set_option(npr_ctx *c, int option, int value) {
       c->sparse_mode = value;
       return NPR_OK;
     case NPR_OPT_SPARSE_CAP:  // Ok-flow slots per lane (0 = the default)
-      if (value < 0 || value > 64) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE_CAP: 0 .. 64");
+      if (value < 0 || value > (int)npr::kSparseCapMax) return fail(c, NPR_ERR_ARG, "NPR_OPT_SPARSE_CAP: 0 .. 128");
       c->sparse_cap = (uint32_t)value;
       return NPR_OK;
     case NPR_OPT_STREAM_CHUNK:  // KiB; 0 = stage the whole capture first

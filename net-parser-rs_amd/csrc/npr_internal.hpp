@@ -158,7 +158,8 @@ struct SparseLane {  // one lane range's walk (k_sparse_walk; rewritten exact by
   uint64_t exit;     // chain position after the range, or the incomplete record (chain END)
   uint32_t cnt, ok;  // records / Ok flows
   uint64_t ovf;      // the first record without a slot (record `cap`; ~0: every record has one)
-  uint64_t okmask;   // bit k: record k (slot k) is an Ok flow
+  uint64_t okmask;   // bit k: record k (slot k) is an Ok flow, k < 64
+  uint64_t okmask2;  // ... bit k - 64 for 64 <= k < 128
 };
 struct SparsePre {   // exact chain state before a 64-lane group (k_sparse_scan -> k_sparse_rows)
   uint64_t exit, cnt, ok, pad;
@@ -184,6 +185,7 @@ struct SparseParams {
 };
 constexpr uint64_t sparse_scan_words(uint64_t ngroups) { return 7 * ngroups + 2; }
 hipError_t launch_sparse(const SparseParams &sp, hipStream_t s);
-constexpr uint32_t kSparseCapDefault = 64;  // slots per lane (<= 64: one mask word)
+constexpr uint32_t kSparseCapDefault = 96;  // slots per lane (<= kSparseCapMax: two mask words)
+constexpr uint32_t kSparseCapMax = 128;
 
 }  // namespace npr

@@ -355,7 +355,10 @@ __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 
   r1 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
 }
 // every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
-// wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded
+// wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded (Ok flows
+// only, densely, measured slower: lanes' slot indices drift apart at the first failed record, and
+// C3's walk went 479 -> 505 us); two mask words of the Ok ones, 96 slots (64: C3's 61-record lanes
+// overflowed into re-walks, rows 125 -> 111 us, walk 479 -> 489 us)
 // Slots and rows are plain (write-back) stores: non-temporal and write-through (sc1, sc0 sc1)
 // stores measured slower for both the scattered slot rows and the whole-line row blocks (DESIGN.md
 // §3.8)
@@ -364,7 +367,7 @@ __device__ __forceinline__ void row_store(u32x4 *d, u32x4 v) { *d = v; }
 struct AreaSink {
   u32x4 *slot0;  // the lane's slot 0 (its first 16 B); NULL: count only
   uint32_t cap, n, okn;
-  uint64_t okmask, ovf;
+  uint64_t okmask, okmask2, ovf;
   __device__ __forceinline__ void operator()(uint64_t p, bool ok, const FlowWords &f) {
     if (n < cap) {
       if (slot0) {
@@ -373,7 +376,8 @@ struct AreaSink {
         slot_store(slot0 + (uint64_t)n * 128u, r0);
         slot_store(slot0 + (uint64_t)n * 128u + 1u, r1);
       }
-      okmask |= (uint64_t)ok << n;
+      if (n < 64) okmask |= (uint64_t)ok << n;
+      else okmask2 |= (uint64_t)ok << (n - 64u);
     } else if (n == cap) {
       ovf = p;
     }
@@ -452,10 +456,10 @@ __global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(4))) v
     }
   }
   uint32_t cnt = 0;
-  AreaSink sink{slot_base(sp, g, lane), sp.cap, 0u, 0u, 0ull, kNone};
+  AreaSink sink{slot_base(sp, g, lane), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
   uint64_t exit = 0;
   if (entry != kNone) exit = lane_walk(kp, row, entry, hi, cnt, sink);
-  SparseLane L{entry, exit, cnt, sink.okn, sink.ovf, sink.okmask};
+  SparseLane L{entry, exit, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
   if (act) sp.lanes[li] = L;
   // the group's aggregate: every link consistent (no END before the last lane, no lane a record
   // spans) -> two wave sums; otherwise the serial monoid
@@ -521,15 +525,15 @@ __device__ void resolve_group(const SparseParams &sp, uint32_t w, Seg s, uint32_
     if (s.exit < sp_end(sp, s.last)) break;  // the chain ended before this lane
     SparseLane L = sp.lanes[li];
     if (s.exit >= hi) {  // a record spans the lane
-      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone, 0ull};
+      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone, 0ull, 0ull};
       s.last = (int64_t)li;
       continue;
     }
     if (L.entry != s.exit) {  // mis-speculated: the exact walk from the incoming position
       uint32_t cnt = 0;
-      AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, kNone};
+      AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
       const uint64_t ex = lane_walk(kp, row, s.exit, hi, cnt, sink);
-      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf, sink.okmask};
+      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
       sp.lanes[li] = L;
       ++rewalks;
     }
@@ -881,7 +885,7 @@ constexpr uint32_t kRowPer = kRowChunk * 128u / kSpBlock;  // 16-B slot chunks p
 __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   __shared__ uint32_t opre[65];
   __shared__ uint32_t okl[64], sl[64];  // Ok flows of the lane, in its slots
-  __shared__ uint64_t ovf[64], hil[64], msk[64];
+  __shared__ uint64_t ovf[64], hil[64], msk[64], msk2[64];
   __shared__ uint32_t kmax_sh;
   __shared__ __attribute__((aligned(16))) u32x4 stage[kRowChunk * 64 * 2];
   const ParseParams &kp = sp.kp;
@@ -918,15 +922,16 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
     }
     const bool me = (part >> tid) & 1ull;
     const uint32_t ok = me ? L.ok : 0u;
-    const uint64_t m = me ? L.okmask : 0ull;
+    const uint64_t m = me ? L.okmask : 0ull, m2 = me ? L.okmask2 : 0ull;
     const uint32_t ex = excl_scan_u32(ok);
     opre[tid] = ex;
     okl[tid] = ok;
     msk[tid] = m;
-    sl[tid] = (uint32_t)__builtin_popcountll(m);
+    msk2[tid] = m2;
+    sl[tid] = (uint32_t)__builtin_popcountll(m) + (uint32_t)__builtin_popcountll(m2);
     ovf[tid] = L.ovf;
     hil[tid] = hi;
-    uint32_t km = m ? 64u - (uint32_t)__builtin_clzll(m) : 0u;
+    uint32_t km = m2 ? 128u - (uint32_t)__builtin_clzll(m2) : m ? 64u - (uint32_t)__builtin_clzll(m) : 0u;
     for (int o = 32; o > 0; o >>= 1) km = max(km, (uint32_t)__shfl_xor((int)km, o));
     if (tid == 63) opre[64] = ex + ok;
     if (tid == 0) kmax_sh = km;
@@ -935,13 +940,15 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   const uint32_t kmax = kmax_sh;
   const uint64_t O = sp.pre[w].ok;
   const uint32_t j = tid >> 2, sub = tid & 3u;
-  const uint64_t mj = msk[j];
+  const uint64_t mj = msk[j], mj2 = msk2[j];
   const uint32_t pj = opre[j];
+  const uint32_t c0j = (uint32_t)__builtin_popcountll(mj);  // Ok flows of lane j in slots 0 .. 63
   // the slots this thread stages are always lane (tid >> 1) & 63's (q = tid + 256 u): a later chunk
   // loads a slot row's 16-B chunk only when one of the four lanes sharing its 128-B line has an Ok
   // flow there (C3's rows kernel read 313 MB for 256 MB of slots before)
   const uint32_t lq = ((tid >> 1) & 63u) & ~3u;
   const uint64_t lmask = msk[lq] | msk[lq + 1] | msk[lq + 2] | msk[lq + 3];
+  const uint64_t lmask2 = msk2[lq] | msk2[lq + 1] | msk2[lq + 2] | msk2[lq + 3];
   for (uint32_t k0 = 0; k0 < kmax; k0 += kRowChunk) {
     const uint32_t nk = kmax - k0 < kRowChunk ? kmax - k0 : kRowChunk;
 #pragma unroll
@@ -957,14 +964,18 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
       for (uint32_t u = 0; u < kRowPer; ++u) {
         const uint32_t q = tid + u * kSpBlock;
         const uint32_t kk = k1 + (q >> 7);
-        v[u] = q < nk1 * 128u && ((lmask >> kk) & 1ull) ? area[(uint64_t)k1 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
+        const bool need = kk < 64u ? ((lmask >> kk) & 1ull) : ((lmask2 >> (kk - 64u)) & 1ull);
+        v[u] = q < nk1 * 128u && need ? area[(uint64_t)k1 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
       }
     }
 #pragma unroll
     for (uint32_t m = 0; m < kRowChunk / 4; ++m) {
       const uint32_t k = k0 + sub + 4 * m;
-      if (k < k0 + nk && ((mj >> k) & 1ull)) {
-        const uint64_t gi = O + pj + (uint32_t)__builtin_popcountll(mj & ((1ull << k) - 1ull));
+      const bool okk = k < 64u ? ((mj >> k) & 1ull) : ((mj2 >> (k - 64u)) & 1ull);
+      if (k < k0 + nk && okk) {
+        const uint32_t below = k < 64u ? (uint32_t)__builtin_popcountll(mj & ((1ull << k) - 1ull))
+                                       : c0j + (uint32_t)__builtin_popcountll(mj2 & ((1ull << (k - 64u)) - 1ull));
+        const uint64_t gi = O + pj + below;
         if (gi < kp.flow_cap) {
           const uint32_t q = ((k - k0) * 64u + j) * 2u;
           put_row(kp, kp.flow_cap - 1 - gi, stage[q], stage[q + 1]);

@@ -181,12 +181,14 @@ def test_kat_frames_as_records(name):
 # ---- synthetic corpora ---------------------------------------------------------------------
 # resident_w16 / _w48: whole 16-wave workgroups (one and three), long ranges with deferred tiles
 # sparse: the sparse record walk forced; _s256: 256-B lane ranges (records span many lanes, most
-# lanes speculate inside payloads); _s4096_c2: two Ok-flow slots per lane (the overflow walk)
+# lanes speculate inside payloads); _s4096_c2: two Ok-flow slots per lane (the overflow walk);
+# _s16384: 16-KiB lanes of short records (up to ~200 per lane: slots past 64 in the second mask word,
+# and the overflow walk past the default 96 slots)
 LIGHT = pytest.mark.parametrize("light", [False, True, 7, 100, 16, 48, "decode",
-                                          "sparse", "sparse_s256", "sparse_s4096_c2"],
+                                          "sparse", "sparse_s256", "sparse_s4096_c2", "sparse_s16384"],
                                 ids=["full", "resident", "resident_w7", "resident_w100", "resident_w16",
                                      "resident_w48", "two_pass",
-                                     "sparse", "sparse_s256", "sparse_s4096_c2"])
+                                     "sparse", "sparse_s256", "sparse_s4096_c2", "sparse_s16384"])
 
 
 @LIGHT
