@@ -40,7 +40,8 @@ struct npr_ctx {
   uint64_t stamp_tiles = 0;
   DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
   int resident = 1;        // NPR_OPT_RESIDENT
-  uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
+  uint32_t res_waves = 0;
+  int cus = 0;             // compute units of the device (0: not queried yet)  // persistent waves of the resident single pass (0: not queried yet)
   bool res_pack = false;   // chained(): its links pack sparse tiles into kept rounds
   int last_pass = 0;       // npr_ctx_last_pass
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
@@ -241,8 +242,9 @@ npr_status sparse_choice(npr_ctx *c, const void *input, uint64_t start, uint64_t
   // lanes took 0.636–0.716 ms in step with that maximum (3 workgroups on some CUs and 2 on others:
   // 0.716; 2 or 3 on every CU: 0.636), profiles/r04_c3_span_sweep.json.
   if (mean && stop > start) {
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) == hipSuccess && cus > 0) {
+    if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+    const int cus = c->cus;
+    if (cus > 0) {
       const uint64_t range = stop - start, est = range / mean, slots = (uint64_t)cus * kSparseCuLanes;
       if (est >= 24 * slots) {
         const uint64_t k = (est + slots * kSparseLaneRecords - 1) / (slots * kSparseLaneRecords);
