@@ -40,8 +40,8 @@ struct npr_ctx {
   uint64_t stamp_tiles = 0;
   DevBuf srec;             // pass-1 record offsets: kMaxRec u16 per tile
   int resident = 1;        // NPR_OPT_RESIDENT
-  uint32_t res_waves = 0;
-  int cus = 0;             // compute units of the device (0: not queried yet)  // persistent waves of the resident single pass (0: not queried yet)
+  uint32_t res_waves = 0;  // persistent waves of the resident single pass (0: not queried yet)
+  int cus = 0;             // compute units of the device (0: not queried yet)
   bool res_pack = false;   // chained(): its links pack sparse tiles into kept rounds
   int last_pass = 0;       // npr_ctx_last_pass
   DevBuf chain;            // npr_dev_parse_extract_chunked: two alternating intermediate summaries
