@@ -82,6 +82,12 @@ class Context:
         msg = self.lib.npr_ctx_last_error(self.handle).decode()
         raise DeviceError(f"status {st}: {msg}")
 
+    def release_stream(self, stream):
+        """npr_stream_release: call before destroying a HIP stream (a raw handle, or an object with
+        `cuda_stream`) that was passed to any device call; torch's pooled streams are never destroyed."""
+        h = getattr(stream, "cuda_stream", stream)
+        self.check(self.lib.npr_stream_release(self.handle, ctypes.c_void_p(h)))
+
     def close(self):
         if getattr(self, "handle", None):
             self.lib.npr_ctx_destroy(self.handle)

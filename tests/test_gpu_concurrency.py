@@ -108,7 +108,7 @@ def test_stream_release_before_destroy():
     a.launch(buf, start=24, stream=torch.cuda.ExternalStream(raw.value, device=dev))
     sm = a.check()  # (on the launch's stream: before it is destroyed)
     assert (sm.n_records, sm.n_flows, sm.consumed) == (nr, nr, cons) and a.flows_np().tobytes() == want
-    a.ctx.check(a.ctx.lib.npr_stream_release(a.ctx.handle, raw))
+    a.ctx.release_stream(raw.value)
     assert hip.hipStreamDestroy(raw) == 0
     s = torch.cuda.Stream(dev)
     b.launch(buf, start=24, stream=s)
