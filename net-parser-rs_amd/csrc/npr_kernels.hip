@@ -1997,13 +1997,15 @@ __global__ __launch_bounds__(kBlock) void k_flow_detail(const uint8_t *buf, uint
   const npr_record rc = load_record(recs, i);
   const uint64_t off = rc.offset + 16;
   uint32_t st = 0xffu;  // the record does not lie inside the buffer
-  volatile uint64_t scratch_d = 0;
-  volatile uint64_t *dp = detail ? detail + i : &scratch_d;  // decode stores the payload here
-  *dp = 0;
+  // (the payload goes straight to detail[i]: a private stand-in for a null `detail` put the pointer
+  // in the flat address space and gave the kernel a scratch segment)
   if (off <= len && len - off >= rc.actual_length) {
     const GlobalReader r{buf + off, len - off};
     FlowWords f;
-    st = decode<false, GlobalReader, true>(r, rc.actual_length, f, dp);
+    st = detail ? decode<false, GlobalReader, true>(r, rc.actual_length, f, detail + i)
+                : decode<false, GlobalReader, false>(r, rc.actual_length, f);
+  } else if (detail) {
+    detail[i] = 0;
   }
   if (status) status[i] = (uint8_t)st;
 }

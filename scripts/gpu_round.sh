@@ -7,6 +7,7 @@
 #          reads those as roofline.traffic)
 #   bench  the bench lines (C2 headline with cpu_baseline, C3, C4 at N=1), rocprofv3 --kernel-trace
 #          --stats summaries of the C2 and C3 bench commands, the per-record API bench
+#   sharded  the C4 bench through the N > 1 path at N = 1 (--sharded)
 # Usage: gpu_round.sh TAG PHASE...
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; R=$(pwd); mkdir -p gpurun_out
@@ -26,11 +27,15 @@ for PHASE in "$@"; do
     timeout -k 10 300 python bench.py --steps 50 --warmup 10 > "gpurun_out/${TAG}_bench.json" 2> "gpurun_out/${TAG}_bench.err" || exit $?
     timeout -k 10 300 python bench.py --config c3 --steps 10 --warmup 2 > "gpurun_out/${TAG}_bench_c3.json" 2>> "gpurun_out/${TAG}_bench.err" || exit $?
     timeout -k 10 300 python bench.py --config c4 --steps 20 --warmup 5 --no-cpu > "gpurun_out/${TAG}_bench_c4.json" 2>> "gpurun_out/${TAG}_bench.err" || exit $?
+    timeout -k 10 300 python bench.py --config c4 --sharded --steps 20 --warmup 5 --no-cpu > "gpurun_out/${TAG}_bench_c4_sharded.json" 2>> "gpurun_out/${TAG}_bench.err" || exit $?
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof" -o run --output-format csv \
        -- python3 "$R/bench.py" --steps 50 --warmup 10 --no-cpu > "$R/gpurun_out/${TAG}_prof.log" 2>&1) || exit $?
     (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/${TAG}_prof_c3" -o run --output-format csv \
        -- python3 "$R/bench.py" --config c3 --steps 10 --warmup 2 --no-cpu > "$R/gpurun_out/${TAG}_prof_c3.log" 2>&1) || exit $?
     timeout -k 10 300 python scripts/bench_records_api.py > "gpurun_out/${TAG}_records_api.json" 2>> "gpurun_out/${TAG}_bench.err" || exit $?
+    ;;
+  sharded)  # the N > 1 code path (RCCL communicator, shared-memory exchange, RCCL flow gather) at N = 1
+    timeout -k 10 300 python bench.py --config c4 --sharded --steps 20 --warmup 5 --no-cpu > "gpurun_out/${TAG}_bench_c4_sharded.json" 2> "gpurun_out/${TAG}_sharded.err" || exit $?
     ;;
   *) echo "unknown phase $PHASE"; exit 2 ;;
   esac
