@@ -37,8 +37,11 @@ __device__ __forceinline__ uint32_t win_sum(const uint8_t *buf, uint64_t p, uint
 }
 __device__ __forceinline__ uint32_t lines_of(uint64_t p) { return 1u + ((((p & ~15ull) & 127u) + 80u) > 128u); }
 
-// C chains per lane: lane range [lo, lo + span) cut into C equal parts, walked together
-template <int C>
+// C chains per lane: lane range [lo, lo + span) cut into C equal parts, walked together.
+// ST: 0 no stores; 1 a 32-B slot per window as k_sparse_walk writes them (slot k of lane j: row
+// (g cap + k) 64 + j, two 16-B stores at a 32-B stride); 2 the same bytes as whole 1-KiB blocks
+// (lane j stores 16-B pieces j and 64 + j of the 2-KiB slot row)
+template <int C, int ST = 0>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_chain(const uint8_t *buf, uint64_t span,
                                                                                         uint64_t nlanes, unsigned long long *out) {
   const uint64_t l = (uint64_t)blockIdx.x * 256u + threadIdx.x;
@@ -61,6 +64,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
         acc += win_sum(buf, pos[c], w0);
         lines += lines_of(pos[c]);
         ++n;
+        if (ST) {
+          u32x4 *slots = reinterpret_cast<u32x4 *>(out + 4);
+          const uint64_t g = l >> 6, j = l & 63u, k = n < 96u ? n - 1u : 95u;
+          u32x4 *row = slots + (g * 96u + k) * 128u;
+          const u32x4 x = u32x4{acc, w0, n, lines};
+          if (ST == 1) {
+            row[2 * j] = x;
+            row[2 * j + 1] = x;
+          } else {
+            row[j] = x;
+            row[64 + j] = x;
+          }
+        }
         pos[c] += 16u + 64u + (w0 % 1441u);
         live = true;
       }
@@ -115,7 +131,8 @@ int main(int argc, char **argv) {
   uint8_t *buf;
   unsigned long long *out;
   CK(hipMalloc(&buf, bytes));
-  CK(hipMalloc(&out, 3 * sizeof(unsigned long long)));
+  const uint64_t slot_bytes = ((nlanes + 63) / 64) * 96ull * 2048ull;
+  CK(hipMalloc(&out, 32 + slot_bytes));
   // random contents (a cheap device fill: hipMemset of a pattern would make every hop the same)
   {
     std::vector<uint32_t> h(1 << 24);
@@ -149,6 +166,8 @@ int main(int argc, char **argv) {
   };
   run("chain1", k_chain<1>);
   run("chain2", k_chain<2>);
+  run("chain1+slots", k_chain<1, 1>);
+  run("chain1+blocks", k_chain<1, 2>);
   run("indep1", k_indep<1>);
   run("indep2", k_indep<2>);
   run("indep4", k_indep<4>);
