@@ -204,12 +204,14 @@ def stats_dump(ws, bufs, hdr, copies, rank):
     st = (ctypes.c_uint32 * 8)()
     ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
     ntl = ctypes.c_uint64(0)
-    ws.ctx.check(lib.npr_ctx_read_stamps(h, None, 0, ctypes.byref(ntl)))
-    nt = ntl.value
-    stamps = np.zeros(nt * 16, dtype=np.uint64)
-    ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
-    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 16))
+    nt = 0
+    # per-wave stamps exist for the resident pass only (the sparse walk keeps counters, no stamps)
+    if lib.npr_ctx_read_stamps(h, None, 0, ctypes.byref(ntl)) == 0:
+        nt = ntl.value
+        stamps = np.zeros(nt * 16, dtype=np.uint64)
+        ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 16))
     print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} tiles={nt}", file=sys.stderr, flush=True)
     ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
 
