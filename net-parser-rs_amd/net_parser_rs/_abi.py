@@ -46,7 +46,7 @@ OPT_DEVICE_WINDOW = 5  # npr_ctx_set_option: npr_parse_extract_pipelined's devic
 OPT_STREAM_CHUNK = 3  # npr_ctx_set_option: host flows-only parses copy in chunks of N KiB overlapped (0 off, default)
 PASS_TWO_PASS, PASS_RESIDENT, PASS_SPARSE = 1, 2, 8  # npr_ctx_last_pass (4, the removed batched launch, no longer occurs)
 OPT_SPARSE = 6      # npr_ctx_set_option: the sparse record walk (0 auto, 1 never, 2 always, N >= 64 lane bytes)
-OPT_SPARSE_CAP = 7  # npr_ctx_set_option: Ok-flow slots per sparse lane (0 = default 64)
+OPT_SPARSE_CAP = 7  # npr_ctx_set_option: record slots per sparse lane (0 = default 96, at most 128)
 ERR_ARG, ERR_DEVICE, ERR_CAPACITY, ERR_TIMEOUT, ERR_NOMEM = -1, -2, -3, -4, -5
 LITTLE, BIG = 0, 1
 
