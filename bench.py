@@ -269,14 +269,14 @@ def run_sharded(args, dev, local, rank, world):
         print(f"[rank {rank}] no gloo group ({e}); summaries over RCCL", file=sys.stderr, flush=True)
         meta = None
     xchg = None
-    if meta is not None:
-        try:
-            xchg = parallel.ShmExchange(meta)
-        except RuntimeError as e:
-            print(f"[rank {rank}] no shared-memory exchange ({e}); summaries over gloo", file=sys.stderr, flush=True)
     # eight steps in flight, the oldest four finished by ONE host exchange (so a slow exchange, gloo at
     # 8 ranks, is paid once per four parses)
     depth = 8
+    if meta is not None:
+        try:
+            xchg = parallel.ShmExchange(meta, slot_bytes=depth * ws.summary.numel())
+        except RuntimeError as e:
+            print(f"[rank {rank}] no shared-memory exchange ({e}); summaries over gloo", file=sys.stderr, flush=True)
     step = parallel.DeviceShardedParse(ws, buf, base, bounds, file_len, usec_magic=True, ts_ref=1_600_000_000,
                                        meta_group=meta, depth=depth, exchange=xchg)
     metas, live, rounds = step.step()
@@ -321,16 +321,23 @@ def run_sharded(args, dev, local, rank, world):
         torch.cuda.synchronize()
         dist.barrier()
         gms.append((time.perf_counter() - g0) * 1e3)
+    bad = 0.0
     if rank == 0:
-        assert merged.numel() == 32 * n_total
         # rows of the merged table run from the last record to the first: check both ends
-        first = merged[:32].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
-        last = merged[-32:].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
         off = lambda r: int.from_bytes(bytes(r["record_offset"]), "little")
-        assert off(first) == file_len - 80 and off(last) == 24
-    t = torch.tensor([wall, kern_ms, float(np.median(gms))], dtype=torch.float64, device=dev)
+        if merged.numel() != 32 * n_total:
+            bad = 1.0
+        else:
+            first = merged[:32].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
+            last = merged[-32:].cpu().numpy().view(npr._abi.FLOW_DTYPE)[0]
+            bad = 0.0 if off(first) == file_len - 80 and off(last) == 24 else 1.0
+    # the verdict rides on the same collective as the timings: every rank learns it, none waits
+    # in a collective for a rank that stopped
+    t = torch.tensor([wall, kern_ms, float(np.median(gms)), bad], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms, gather_ms = float(t[0]), float(t[1]), float(t[2])
+    if t[3] != 0:
+        raise SystemExit(f"[rank {rank}] the merged flow table on rank 0 is not the capture's")
     out = base_line(args, world, wall, R, len(buf))
     out["config"].update({"records_per_gpu": R, "capture_bytes": file_len, "parallelism": f"record-range x{world}"})
     out["roofline"] = roofline(80 * R, 32 * R, kern_ms, stream_b=80 * R)
@@ -388,16 +395,10 @@ def _rank_entry(rank, world, port, argv):
 
 def spawn_ranks(args, argv):
     """`python bench.py --gpus N` with no launcher: start N rank processes (one per GPU) before this
-    process touches any GPU, as torch.distributed.run would, and exit with the worst exit code."""
-    import multiprocessing as mp
-    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's state is inherited
+    process touches any GPU, as torch.distributed.run would, and exit with the worst exit code.  A
+    rank that fails ends the others (parallel.supervise_ranks), so none waits in a collective."""
     port = _free_port()
-    procs = [ctx.Process(target=_rank_entry, args=(r, args.gpus, port, argv)) for r in range(args.gpus)]
-    for p in procs:
-        p.start()
-    for p in procs:
-        p.join()
-    codes = [p.exitcode for p in procs]
+    codes = parallel.supervise_ranks(_rank_entry, [(r, args.gpus, port, argv) for r in range(args.gpus)])
     bad = [c for c in codes if c != 0]
     if bad:
         print(f"bench.py: rank exit codes {codes}", file=sys.stderr, flush=True)

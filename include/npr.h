@@ -272,6 +272,14 @@ npr_status npr_ctx_set_option(npr_ctx *ctx, int option, int value);
  * counterpart): 0 none yet, 1 the two-pass kernels, 2 the resident single pass, 8 the sparse
  * record walk (4, a batched resident launch, is no longer produced). */
 int npr_ctx_last_pass(const npr_ctx *ctx);
+/* The flows-only device parse chooses its pass (and its link sizes) by the record density of the
+ * capture's first 256 KiB, remembered per (device address, start, stop, byte order) so that a
+ * capture parsed again costs no probe.  Call this when new bytes replace a capture at the same
+ * address (NULL: forget every capture).  Without the call the choice still follows the bytes one
+ * parse late: npr_dev_check corrects a remembered density that is more than 2x off the parse's own.
+ * The host entry points forget their staging buffer's density whenever they stage new bytes.
+ * The choice never changes a result, only the time. */
+npr_status npr_ctx_forget_density(npr_ctx *ctx, const void *input);
 /* Bytes of device workspace the next parse of `len` bytes needs (tile hand-off slots). */
 uint64_t npr_workspace_bytes(uint64_t len);
 

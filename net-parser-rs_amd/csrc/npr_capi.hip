@@ -73,11 +73,15 @@ struct npr_ctx {
   uint64_t sparse_span = 0;
   DevBuf sparse;
   // record density of recently probed captures (device pointer, range, byte order -> bytes per
-  // record): the choice of pass never changes a result, so a stale entry only costs time
+  // record): the choice of pass never changes a result, so a stale entry only costs time.  An entry
+  // goes when the host stages new bytes at that address (stage_input), when the caller says the
+  // bytes changed (npr_ctx_forget_density), and it is corrected from the parse's own summary when
+  // npr_dev_check reads one whose density disagrees (the next call then chooses by the new bytes)
   struct Probe {
     const void *input = nullptr;
     uint64_t start = 0, stop = 0, mean = 0;
     int e = -1;
+    const npr_summary *sum = nullptr;  // the summary of the last parse that chose by this entry
   };
   Probe probes[8];
   uint32_t probe_next = 0;
@@ -214,7 +218,27 @@ npr_status probe_density(npr_ctx *c, const void *input, uint64_t start, uint64_t
   pr.stop = stop;
   pr.e = (int)e;
   pr.mean = mean;
+  pr.sum = nullptr;
   return NPR_OK;
+}
+// The parse whose summary is `sum` chose its pass by the entry for (input, start, stop, e).
+void probe_note(npr_ctx *c, const void *input, uint64_t start, uint64_t stop, npr_endianness e, const npr_summary *sum) {
+  for (auto &pr : c->probes)
+    if (pr.input == input && pr.start == start && pr.stop == stop && pr.e == (int)e) pr.sum = sum;
+}
+// Forget the density of the capture at `input` (nullptr: of every capture).
+void probe_forget(npr_ctx *c, const void *input) {
+  for (auto &pr : c->probes)
+    if (!input || pr.input == input) pr = npr_ctx::Probe{};
+}
+// npr_dev_check read summary `h` (written to `sum`): an entry that chose by a density more than 2x
+// off the parse's own (records and bytes consumed) takes the parse's.
+void probe_correct(npr_ctx *c, const npr_summary *sum, const npr_summary &h) {
+  for (auto &pr : c->probes) {
+    if (!pr.input || pr.sum != sum || h.n_records < 16 || h.consumed <= pr.start) continue;
+    const uint64_t got = (h.consumed - pr.start) / h.n_records;
+    if (got > 2 * pr.mean || 2 * got < pr.mean) pr.mean = got;
+  }
 }
 bool sparse_forced(const npr_ctx *c) { return c->sparse_mode == 2 || c->sparse_mode >= 64; }
 // Lane-range bytes of the sparse record walk for a flows-only parse of records starting in
@@ -337,6 +361,11 @@ extern "C" {
 
 const char *npr_version(void) { return NPR_VERSION_STRING; }
 int npr_ctx_last_pass(const npr_ctx *c) { return c ? c->last_pass : 0; }
+npr_status npr_ctx_forget_density(npr_ctx *c, const void *input) {
+  if (!c) return NPR_ERR_ARG;
+  probe_forget(c, input);
+  return NPR_OK;
+}
 int npr_abi_version(void) { return NPR_ABI_VERSION; }
 
 // elements per level: [0] tiles, [l] = ceil([l-1] / 64)
@@ -551,6 +580,7 @@ npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, ui
     if (st) return st;
     uint64_t span = 0;  // long records: the sparse walk, one launch set for any size
     if ((st = sparse_choice(c, input, start, len, e, true, stream, span))) return st;
+    probe_note(c, input, start, len, e, o->summary);
     if (span) {
       SpanScope scope{c};
       c->sparse_span = span;
@@ -625,6 +655,7 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
   if (st) return st;
   uint64_t span = 0;  // long records: sparse links (chunk_bytes 0: one sparse launch set for the range)
   if ((st = sparse_choice(c, input, start, stop, e, !speculative_start && !sh, stream, span))) return st;
+  if (!speculative_start && !sh) probe_note(c, input, start, stop, e, o->summary);
   SpanScope span_scope{c};
   if (span) {
     c->sparse_span = span;
@@ -865,6 +896,7 @@ npr_status npr_dev_check(npr_ctx *c, const npr_dev_outputs *o, void *stream, npr
   HIP_CHECK(c, hipStreamSynchronize(s));
   if (hs) *hs = *c->summary_h;
   const uint32_t want = summary_epoch(c, o->summary);  // the launch that wrote this summary
+  if (c->summary_h->epoch == (want ? want : c->epoch)) probe_correct(c, o->summary, *c->summary_h);
   if (c->summary_h->epoch != (want ? want : c->epoch)) {
     return fail(c, NPR_ERR_TIMEOUT, "parse did not complete (tile hand-off timed out)");
   }
@@ -981,6 +1013,7 @@ static bool small_call(size_t len, size_t n) { return len + n * sizeof(npr_recor
 static npr_status stage_input(npr_ctx *c, const uint8_t *in, size_t len) {
   npr_status st = ensure(c, c->in, len + 16);
   if (st) return st;
+  probe_forget(c, c->in.p);  // new bytes at the staging address: its density is probed afresh
   if (len) HIP_CHECK(c, hipMemcpyAsync(c->in.p, in, len, hipMemcpyHostToDevice, c->stream));
   return NPR_OK;
 }
@@ -997,6 +1030,7 @@ static npr_status stream_parse(npr_ctx *c, const uint8_t *in, size_t len, uint64
   const uint64_t nchunks = (len + chunk - 1) / chunk;
   npr_status st = ensure(c, c->in, len + 16);
   if (st) return st;
+  probe_forget(c, c->in.p);
   if ((st = ensure(c, c->chain, 2 * sizeof(npr_summary), true))) return st;
   if (!c->copy_stream) HIP_CHECK(c, hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
   while (c->copied.size() < nchunks) {

@@ -185,7 +185,7 @@ __device__ __forceinline__ Seg prefix_seg(uint64_t e0, uint64_t e1, uint64_t e2,
 // Fold lanes [lo .. 0] (ascending tile order = descending lane) into one segment.  Fast path:
 // every link consistent, no END, no pass-through, all valid -> two wave sums; otherwise the
 // serial monoid (wave-uniform, readlane).
-__device__ Seg fold_window(const ParseParams &kp, const LaneSeg &L, int lo) {
+__device__ __forceinline__ Seg fold_window(const ParseParams &kp, const LaneSeg &L, int lo) {
   const int lane = (int)(threadIdx.x & 63u);
   const uint64_t prev_exit = shfl_down64(L.exit);  // exit of the preceding segment (lane + 1)
   const bool inr = lane <= lo;
@@ -481,7 +481,14 @@ __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, u
   // pair, v_alignbyte + readfirstlane, and three compare-and-branch exits; the srec address walks
   // in a VGPR.  Both LDS pointers come from __shared__ arrays (every walk_tile caller's).
   uint32_t va, vd, vlo, vhi, t;
-  const uint32_t sa = lds_addr(srec) + 2u * n, wb = lds_addr(w);
+  // every operand wave-uniform by construction; readfirstlane makes that visible where the
+  // compiler's uniformity analysis loses track (the asm takes them in scalar registers)
+  const uint32_t sa = __builtin_amdgcn_readfirstlane(lds_addr(srec) + 2u * n);
+  const uint32_t wb = __builtin_amdgcn_readfirstlane(lds_addr(w));
+  r = __builtin_amdgcn_readfirstlane(r);
+  n = __builtin_amdgcn_readfirstlane(n);
+  incl = __builtin_amdgcn_readfirstlane(incl);
+  hop_span = __builtin_amdgcn_readfirstlane(hop_span);
 #define NPR_HOP_ASM(PERM)                                                                              \
   asm volatile(                                                                                        \
       "v_mov_b32 %[va], %[sa]\n"                                                                       \
@@ -520,7 +527,7 @@ __device__ __forceinline__ uint32_t hop_run(const uint32_t *w, uint16_t *srec, u
   return r;
 }
 
-__device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
+__device__ __forceinline__ uint64_t walk_tile_inl(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
                               uint64_t tile_hi, uint64_t entry, uint32_t &n_out, uint32_t *last_io = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const bool big = kp.big;
@@ -596,6 +603,12 @@ __device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t
   if (last_io) *last_io = last;
   return exit_far != kNone ? exit_far : tile_lo + r;
 }
+// (the resident pass inlines walk_tile_inl: a call there keeps its length state in scratch
+// memory; the two-pass kernels call this out-of-line copy, which keeps their registers free)
+__device__ uint64_t walk_tile(const ParseParams &kp, const uint32_t *w, uint16_t *srec, uint64_t tile_lo,
+                              uint64_t tile_hi, uint64_t entry, uint32_t &n_out, uint32_t *last_io = nullptr) {
+  return walk_tile_inl(kp, w, srec, tile_lo, tile_hi, entry, n_out, last_io);
+}
 
 // diagnostics (DIAG kernel variants only: the production kernels carry none of this)
 struct Stamps {  // kept in registers, written once at the end (a store per stamp would make
@@ -613,10 +626,12 @@ __device__ __forceinline__ void stamp_flush(const ParseParams &kp, const Stamps 
 // First strong (else first weak) record start in [lo, span) of the staged tile; kNone if
 // neither (wave-uniform).  64 candidates per round are screened on their own header (one
 // 16-B read per lane); only the survivors, in offset order, have their chain graded.
-__device__ uint64_t speculate(SpecCtx sc, const ParseParams &kp, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
+// (the capture's length by value, not the ParseParams: a by-reference kernel argument reaching a
+// call the compiler does not inline is copied to scratch memory first)
+__device__ uint64_t speculate(SpecCtx sc, uint64_t len, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
                               uint32_t span) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t avail = kp.len - tile_lo;
+  const uint64_t avail = len - tile_lo;
   sc.avail = avail > 0xffffffffull ? 0xffffffffu : (uint32_t)avail;
   sc.exact_end = avail <= 0xffffffffull;
   uint32_t weak = 0xffffffffu;
@@ -734,7 +749,7 @@ __global__ __launch_bounds__(kWave) void k_count_tiles(ParseParams kp) {
   if (!known) {
     const SpecCtx sc = spec_ctx(kp, scb);
     const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;  // a range starts at `start`
-    entry = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+    entry = tile_hi > tile_lo + lo ? speculate(sc, kp.len, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
     if (DIAG && kp.stats && lane == 0 && entry == kNone) atomicAdd(kp.stats + kStatNoEntry, 1u);
   }
   entry = uni64(entry);
@@ -1091,7 +1106,7 @@ __device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int6
 }
 
 // fold `cnt` (1..64) consecutive level-`lvl` elements from `base` (bounded wait for all)
-__device__ bool res_fold(const ParseParams &kp, int lvl, int64_t base, int cnt, Seg &out, uint64_t t0) {
+__device__ __forceinline__ bool res_fold(const ParseParams &kp, int lvl, int64_t base, int cnt, Seg &out, uint64_t t0) {
   const int lane = (int)(threadIdx.x & 63u);
   const bool inr = lane < cnt;
   const int64_t last = base + cnt - 1;
@@ -1116,7 +1131,7 @@ __device__ __forceinline__ uint32_t res_arrive(uint32_t *ctr) {
 // Fold a window of `size` children held one per lane (ascending lane = ascending order): each
 // lane's exclusive prefix inside the window (lane 0: none) and the window's aggregate (the chain-
 // consistency monoid; fast path: every link consistent -> two exclusive scans).
-__device__ void res_fold_lanes(const ParseParams &kp, const LaneSeg &L, int size, Seg &ep, Seg &agg) {
+__device__ __forceinline__ void res_fold_lanes(const ParseParams &kp, const LaneSeg &L, int size, Seg &ep, Seg &agg) {
   const int lane = (int)(threadIdx.x & 63u);
   const bool inr = lane < size;
   const uint64_t prev_exit = shfl_up64(L.exit);
@@ -1189,7 +1204,7 @@ __device__ __forceinline__ Seg res_prefix_seg(const ParseParams &kp, uint64_t *e
 
 // exact chain state before wave v, from X = E(b) ⊕ (prefix inside the workgroup) when that is
 // flagged: contradictions settled by exact prefixes P(m), then aggregates (G(b) where aligned)
-__device__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t0) {
+__device__ __forceinline__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t0) {
   const uint32_t lane = threadIdx.x & 63u;
   if (X.valid) return true;
   // a mis-speculated range m < v: from its exact prefix on, aggregates (G1 where aligned)
@@ -1282,7 +1297,7 @@ __device__ __forceinline__ void res_put_v6(const ParseParams &kp, uint64_t o, co
 
 // Re-read tiles [t0, c1) of the range from the exact chain position `pos` (counts pcnt / pok
 // before it): walk, decode, write every Ok flow.  Returns the exit; updates the counts.
-__device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_from, uint32_t c1, uint64_t pos,
+__device__ __forceinline__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_from, uint32_t c1, uint64_t pos,
                              uint64_t &cnt, uint64_t &ok) {
   const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
@@ -1300,7 +1315,7 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
     const uint32_t *w = sh.data[slot];
     if (!ended && pos >= tile_lo && pos < tile_hi) {
       uint32_t n = 0;
-      const uint64_t ex = uni64(walk_tile(kp, w, sh.srec, tile_lo, tile_hi, pos, n, &wlast));
+      const uint64_t ex = uni64(walk_tile_inl(kp, w, sh.srec, tile_lo, tile_hi, pos, n, &wlast));
       wave_sync();
       uint32_t okbase = 0;
       for (int s = 0; s < kRounds; ++s) {
@@ -1330,6 +1345,55 @@ __device__ uint64_t res_emit(const ParseParams &kp, ResShared &sh, uint32_t t_fr
     wave_sync();  // done with this slot before it is refilled
   }
   return pos;
+}
+
+// The kept rounds' Ok flows to rows flow_cap - 1 - (x0 + Ok rank), x0 = the exact Ok flows before
+// the wave (phase B).  Each round's Ok rows are one contiguous
+// block: staged in the wave's idle ring slot in address order, then stored as contiguous 16-B chunks
+// (lane i: chunks i and 64 + i), so each store instruction writes whole lines, written through (sc1)
+// through a buffer resource over exactly the block (its range check drops the chunks past 2 nok).
+// A write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane rounds
+// (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s; write-through
+// measured 28.1-28.5 us per C2 launch against 30.3-30.7 us non-temporal (round 3,
+// scripts/gpu_variants.sh), C3 1.443 against 1.478 ms.  Rounds past flow_cap go row by row (res_put).
+template <int NS>
+__device__ __forceinline__ void res_write_kept(const ParseParams &kp, uint32_t *stg_words, const uint32_t (&fl)[NS][8],
+                                               uint32_t ns, uint32_t m_ok, uint32_t m_lo, uint32_t m_hi, uint64_t x0,
+                                               uint64_t base) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) {
+    if ((uint32_t)q < ns) {
+      const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
+      const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
+      const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
+      const uint64_t f0 = x0 + okb;
+      if (nok && f0 + nok <= kp.flow_cap) {
+        const bool mine = (bal >> lane) & 1ull;
+        const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        const uint64_t p = base + fl[q][7];
+        const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
+        u32x4 *stg = reinterpret_cast<u32x4 *>(stg_words);
+        if (mine) {
+          const uint32_t k = nok - 1u - rank;  // rank r lands at row flow_cap - 1 - (f0 + r)
+          stg[stg_slot<128>(2 * k)] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
+          stg[stg_slot<128>(2 * k + 1)] =
+              u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+        }
+        wave_sync();
+        u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
+        const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, (int)(2u * nok * 16u), 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane)], rr, (int)(lane * 16u), 0, kPolSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane + 64)], rr, (int)((lane + 64u) * 16u), 0, kPolSc1);
+        if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
+        wave_sync();  // the slot is rewritten by the next round
+      } else if ((bal >> lane) & 1ull) {
+        const uint64_t fi = x0 + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
+        if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
+      }
+    }
+  }
 }
 
 struct ResWgShared {  // one workgroup's LDS: the waves' rings, then the in-LDS fold
@@ -1381,11 +1445,149 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   uint32_t wlast = kAnyLen;  // incl_len of the last record walked (walk_tile)
   uint64_t wait_ticks = 0;  // DIAG: phase A time spent waiting for tiles to land
   uint64_t walk_ticks = 0;  // DIAG: ... walking the record chain
-  for (uint32_t t = c0; t < c1; ++t) {
+  // ---- phase A, the one-length prefix (dense captures: C2, any capture of one record size) --------
+  // The range's first tiles while every record starting in a tile has the length of the tile's
+  // first record, at most 64 of them, and the capture runs on for a tile past it (so no record of
+  // the tile is incomplete): one header read per lane confirms the tile's records, lane l decodes
+  // record l, and the flows land in kept round k = the tile's index in the range (a compile-time
+  // register block: no per-round dynamic select).  The chain walk, the round bookkeeping and the
+  // loop control of the general loop below cost ~300 SALU + ~270 VALU per C2 tile beside the
+  // decode (PMC); this path issues a fraction of that.  The first tile that does not
+  // qualify goes to the general loop, which continues from the same state (same results).
+  uint32_t t_gen = c0;       // first tile of the general loop
+  bool succ_issued = false;  // the fast prefix already issued that tile's successor's DMA
+  if constexpr (!PACK) {
+    // 32-bit positions relative to the range base (the prefix covers at most kResSlots tiles), one
+    // buffer resource over the range (bytes past the capture read 0, as dma_tile's do), the
+    // header's byte order as a v_perm selector
+    const uint64_t stop64 = kp.stop - base, len64 = kp.len - base;  // base <= stop <= len
+    const uint32_t stop_r = stop64 < 0xffffffffull ? (uint32_t)stop64 : 0xffffffffu;
+    const uint32_t len_r = len64 < 0x7fff0000ull ? (uint32_t)len64 : 0x7fff0000u;
+    const __amdgpu_buffer_rsrc_t rsr =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(kp.buf + base), 0, (int)((len_r + 15u) & ~15u), 0x00020000);
+    const uint32_t hsel = kp.big ? 0x00010203u : 0x03020100u;
+    const uint32_t l16 = lane * 16u;
+    uint32_t pr = 0;  // the chain position - base, once an entry is known
+    bool go = active && c0 < c1;
+#pragma unroll
+    for (uint32_t Q = 0; Q < (uint32_t)kResSlots; ++Q) {  // (unrolled: kept round Q is a register block)
+      const uint32_t t = c0 + Q;
+      if (!go || t >= c1) break;
+      const uint32_t slot = Q % kResRing;
+      const uint32_t lo_r = Q * (uint32_t)kTile;
+      const uint32_t hi_r = lo_r + (uint32_t)kTile < stop_r ? lo_r + (uint32_t)kTile : stop_r;
+      if (t + 1 < c1) {  // the successor tile's DMA (dma_tile's rows, offsets into the range)
+        uint32_t *dst = sh.w[wid].data[(slot + 1) % kResRing];
+#pragma unroll
+        for (int i = 0; i < kRows; ++i) {
+          uint32_t vo;
+          asm volatile("v_add_u32 %0, %1, %2" : "=v"(vo) : "n"(1024 * i + (int)kTile), "v"(l16 + lo_r));
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(rsr, (lds_ptr_t)(dst + i * 256), 16, vo, 0, 0, 2);
+        }
+        uint32_t vh;
+        asm volatile("v_lshrrev_b32 %0, 2, %1\n\tv_add_u32 %0, %2, %0" : "=&v"(vh) : "v"(l16), "v"(lo_r + 2u * (uint32_t)kTile));
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsr, (lds_ptr_t)(dst + kRows * 256), 4, vh, 0, 0, 2);
+      }
+      const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
+      res_wait<0>(t + 1 < c1 ? 1u : 0u);
+      if (DIAG) wait_ticks += __builtin_amdgcn_s_memrealtime() - tw0;
+      const uint32_t *w = sh.w[wid].data[slot];
+      if (Q == 0) {
+        const uint64_t tile_lo = base, tile_hi = base + hi_r;
+        sc = spec_ctx(kp, scb);
+        if (DIAG) stamp_at(st, 1);
+        uint64_t e;
+        if (t == 0 && !spec0) {
+          e = kp.start;
+        } else {
+          const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;
+          e = tile_hi > tile_lo + lo ? speculate(sc, kp.len, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+        }
+        e = uni64(e);
+        if (e != kNone) {
+          entry = pos = e;
+          pr = (uint32_t)(e - base);
+        }
+      }
+      const uint32_t span = hi_r - lo_r;
+      // every record starting in the tile ends inside the capture (no Incomplete test needed)
+      bool fast = pos != kNone && pr >= lo_r && pr < hi_r && len_r - hi_r >= (uint32_t)kTile + 16u;
+      uint32_t r = 0, incl = 0, stride = 16, q = 0, n = 0;
+      bool inb = false;
+      if (fast) {
+        r = pr - lo_r;
+        incl = (uint32_t)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_perm(0u, lds_le32(w, r + 8u), hsel));
+        stride = incl + 16u;
+        fast = incl <= (uint32_t)kTile && span - r <= 64u * stride;
+      }
+      if (fast) {
+        q = r + lane * stride;  // < 2^24: lane < 64, stride <= 16 + kTile
+        inb = q < span;
+        const uint32_t h = __builtin_amdgcn_perm(0u, lds_le32(w, (inb ? q : r) + 8u), hsel);
+        // every record of the tile: the same length (readfirstlane: visibly uniform control flow)
+        fast = __builtin_amdgcn_readfirstlane((int)(__ballot(inb && h != incl) == 0ull)) != 0;
+        n = (uint32_t)__builtin_amdgcn_readfirstlane((int)__builtin_popcountll(__ballot(inb)));
+      }
+      if (!fast) {  // the general loop takes this tile (its successor's DMA is in flight)
+        go = false;
+        t_gen = t;
+        succ_issued = t + 1 < c1;
+        break;
+      }
+      // lane l decodes record l (lanes past the tile's records read record 0: LDS broadcast)
+      const uint32_t rr = inb ? q : r;
+      FlowWords f;
+      const uint32_t stc = decode_fast<true, true>(w, rr + 16u, incl, f, inb);
+      if (__builtin_amdgcn_readfirstlane((int)(__ballot(inb && stc == 0xffu) != 0ull))) {
+        // a frame only the general decode<> handles: the general loop takes the tile
+        go = false;
+        t_gen = t;
+        succ_issued = t + 1 < c1;
+        break;
+      }
+      const uint64_t bal = __ballot(inb && stc == NPR_FLOW_OK);
+      fl[Q][0] = (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) ? f.v6off : f.d[0];
+#pragma unroll
+      for (int j = 1; j < 7; ++j) fl[Q][j] = f.d[j];
+      fl[Q][7] = lo_r + rr;  // record offset - base
+      m_ok = lane == Q ? okc : m_ok;
+      m_lo = lane == Q ? (uint32_t)bal : m_lo;
+      m_hi = lane == Q ? (uint32_t)(bal >> 32) : m_hi;
+      // (loop-carried state made visibly wave-uniform: the general loop's hand-written hop walk
+      // takes it in scalar registers)
+      okc = (uint32_t)__builtin_amdgcn_readfirstlane(okc + (uint32_t)__builtin_popcountll(bal));
+      cnt = (uint32_t)__builtin_amdgcn_readfirstlane(cnt + n);
+      ns = Q + 1;
+      fill = n;
+      wlast = (uint32_t)__builtin_amdgcn_readfirstlane(incl);
+      pr = (uint32_t)__builtin_amdgcn_readfirstlane(lo_r + r + n * stride);  // >= hi_r: the n-th record was the tile's last
+      wave_sync();  // done with this slot before it is refilled
+      if (c1 - c0 <= kStepPrioTiles) {  // (the general loop's priority steps, below)
+        if (Q == 0) __builtin_amdgcn_s_setprio(2);
+        else if (Q == 1) __builtin_amdgcn_s_setprio(1);
+        else if (Q == 2) __builtin_amdgcn_s_setprio(0);
+      } else if ((Q & 3u) == 3u) {
+        if (lane == 0) sh.prog[wid] = Q + 1;
+        uint32_t mn = lane < kResWg ? sh.prog[lane] : ~0u;
+#pragma unroll
+        for (int o = 1; o < (int)kResWg; o <<= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o));
+        const uint32_t d = Q + 1 - __builtin_amdgcn_readfirstlane(mn);
+        if (d == 0) __builtin_amdgcn_s_setprio(3);
+        else if (d == 1) __builtin_amdgcn_s_setprio(2);
+        else if (d == 2) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+      }
+      t_gen = t + 1;
+      succ_issued = false;
+    }
+    if (pos != kNone) pos = uni64(base + pr);
+    static_assert(kResSlots == 6, "one fast tile per kept round");
+  }
+  for (uint32_t t = t_gen; t < c1; ++t) {
     const uint32_t k = t - c0, slot = k % kResRing;
     const uint64_t tile_lo = base + (uint64_t)k * kTile;
     const uint64_t tile_hi = tile_lo + kTile < kp.stop ? tile_lo + kTile : kp.stop;
-    if (t + kResRing - 1 < c1)
+    if (t + kResRing - 1 < c1 && !(succ_issued && t == t_gen))
       dma_tile<2>(kp, tile_lo + (uint64_t)(kResRing - 1) * kTile, sh.w[wid].data[(slot + kResRing - 1) % kResRing]);
     const uint64_t tw0 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
     res_wait<0>(c1 - 1 - t < (uint32_t)(kResRing - 1) ? c1 - 1 - t : (uint32_t)(kResRing - 1));
@@ -1402,7 +1604,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
           e = kp.start;
         } else {
           const uint32_t lo = t == 0 ? (uint32_t)(kp.start - tile_lo) : 0u;
-          e = tile_hi > tile_lo + lo ? speculate(sc, kp, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
+          e = tile_hi > tile_lo + lo ? speculate(sc, kp.len, w, tile_lo, lo, (uint32_t)(tile_hi - tile_lo)) : kNone;
         }
         e = uni64(e);
         if (e != kNone) entry = pos = e;
@@ -1410,7 +1612,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
       if (pos != kNone && pos < tile_hi) {
         uint32_t n = 0;
         const uint64_t tw1 = DIAG ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint64_t ex = uni64(walk_tile(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n, &wlast));
+        const uint64_t ex = uni64(walk_tile_inl(kp, w, sh.w[wid].srec, tile_lo, tile_hi, pos, n, &wlast));
         wave_sync();
         if (DIAG) walk_ticks += __builtin_amdgcn_s_memrealtime() - tw1;
         const uint32_t rounds = (n + 63u) >> 6;
@@ -1625,51 +1827,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   const bool before_end = X.exit < tile_end(kp, X.last);  // the chain ended before this range
   if (!before_end && xe < range_hi && xe >= range_lo) {
     if (entry != kNone && xe == entry) {  // the speculated chain is the exact one: flows from registers
-      if (kp.flows) {
-#pragma unroll
-        for (int q = 0; q < kResSlots; ++q) {
-          if ((uint32_t)q < ns) {
-            const uint32_t okb = __builtin_amdgcn_readlane(m_ok, q);
-            const uint64_t bal = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane(m_hi, q) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane(m_lo, q);
-            // The round's Ok rows are one contiguous block of nok rows: stage them in this wave's idle
-            // ring slot in address order, then store the block as contiguous 16-B chunks (lane i:
-            // chunks i and 64 + i), so each store instruction writes whole lines (written through, below).  A
-            // write-only microbenchmark (scripts/microbench/store_pattern.hip) writes one-row-per-lane
-            // rounds (two stores at a 32-B stride) at 1.5-1.8 TB/s and contiguous ones at 2.4-3.3 TB/s;
-            // in this kernel C2 went 31.3 -> 30.8 us, and non-temporal stores a further 30.6 -> 30.1.
-            const uint32_t nok = (uint32_t)__builtin_popcountll(bal);
-            const uint64_t f0 = xo + okb;
-            if (nok && f0 + nok <= kp.flow_cap) {
-              const bool mine = (bal >> lane) & 1ull;
-              const uint32_t rank = (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-              const uint64_t p = base + fl[q][7];
-              const bool v6 = (fl[q][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-              u32x4 *stg = reinterpret_cast<u32x4 *>(sh.w[wid].data[0]);
-              if (mine) {
-                const uint32_t k = nok - 1u - rank;  // rank r lands at row flow_cap - 1 - (f0 + r)
-                stg[stg_slot<128>(2 * k)] = u32x4{v6 ? 0u : fl[q][0], v6 ? 0u : fl[q][1], fl[q][2], fl[q][3]};
-                stg[stg_slot<128>(2 * k + 1)] =
-                    u32x4{fl[q][4], fl[q][5], fl[q][6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
-              }
-              wave_sync();
-              u32x4 *dst = reinterpret_cast<u32x4 *>(kp.flows + (kp.flow_cap - f0 - nok) * 8);
-              // write-through (sc1) stores through a buffer resource over exactly the block (its range
-              // check drops the chunks past 2 nok): no dirty lines left in the XCD's L2 for the kernel-
-              // end write-back.  Interleaved A/B on one box (scripts/gpu_variants.sh, round 3): C2
-              // 28.1-28.5 us against 30.3-30.7 us non-temporal, C3 1.443 against 1.478 ms
-              const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc((void *)dst, 0, (int)(2u * nok * 16u), 0x00020000);
-              __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane)], rr, (int)(lane * 16u), 0, kPolSc1);
-              __builtin_amdgcn_raw_buffer_store_b128(stg[stg_slot<128>(lane + 64)], rr, (int)((lane + 64u) * 16u), 0, kPolSc1);
-              if (mine && v6) res_put_v6(kp, kp.flow_cap - 1 - (f0 + rank), fl[q], p);
-              wave_sync();  // the slot is rewritten by the next round
-            } else if ((bal >> lane) & 1ull) {
-              const uint64_t fi = xo + okb + (uint32_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-              if (fi < kp.flow_cap) res_put(kp, kp.flow_cap - 1 - fi, fl[q], base + fl[q][7]);
-            }
-          }
-        }
-      }
+      if (kp.flows) res_write_kept<kResSlots>(kp, sh.w[wid].data[0], fl, ns, m_ok, m_lo, m_hi, xo, base);
       if (DIAG) stamp_at(st, 5);
       if (tdef < c1) {
         uint64_t dc = xc + cdef, dok = xo + odef;

@@ -116,7 +116,7 @@ EXPORTED = [
     "npr_dev_parse_extract_chunked", "npr_dev_parse_extract_shard", "npr_dev_check", "npr_dev_extract_flows",
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
     "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch", "npr_shm_all_gather",
-    "npr_stream_release",
+    "npr_stream_release", "npr_ctx_forget_density",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -178,6 +178,7 @@ _SIGNATURES = {
     "npr_dev_flow_details": (ctypes.c_int, [_vp, _vp, ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, _vp, _vp]),
     "npr_dev_parse_extract_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "npr_stream_release": (ctypes.c_int, [_vp, _vp]),
+    "npr_ctx_forget_density": (ctypes.c_int, [_vp, _vp]),
     "npr_shm_all_gather": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
 }
@@ -197,7 +198,11 @@ def load_library(path=None):
             " (the parser has no CPU fallback)")
     lib = ctypes.CDLL(p)
     for name, (res, args) in _SIGNATURES.items():
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:  # an A/B build of an older revision (NPR_LIB) may predate a symbol
+            if p == LIB_PATH:
+                raise ImportError(f"{p} does not export {name}")
+            continue
         fn.restype = res
         fn.argtypes = args
     if path is None:

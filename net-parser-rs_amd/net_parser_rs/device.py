@@ -43,6 +43,11 @@ class Workspace:
         self.ctx.check(st)
         self._stream = s
 
+    def forget_density(self, buf=None):
+        """New bytes replace the capture at `buf`'s address (None: any capture): the next parse probes
+        its record density afresh (npr_ctx_forget_density; the pass choice never changes a result)."""
+        self.ctx.check(self.ctx.lib.npr_ctx_forget_density(self.ctx.handle, buf.data_ptr() if buf is not None else None))
+
     def launch_range(self, buf, start, stop, endianness=_abi.LITTLE, speculative=False, ref_record=24,
                      nbytes=None, stream=None):
         """Records that START in [start, stop) of `buf` (payloads may run past stop): one shard of a

@@ -453,6 +453,12 @@ class DeviceShardedParse:
         # between two parses; the flow rows still go over RCCL
         self.meta_group = meta_group
         self.xchg = exchange if exchange is not None else (GlooExchange(meta_group) if meta_group is not None else None)
+        # finish_steps(n) exchanges n summaries at once: a shared-memory slot must hold `depth` of them
+        # (checked here, before any work is in flight)
+        slot = getattr(self.xchg, "slot_bytes", None)
+        if slot is not None and self.depth * ws.summary.numel() > slot:
+            raise ValueError(f"DeviceShardedParse: depth {self.depth} x {ws.summary.numel()}-B summaries exceed the "
+                             f"exchange's {slot}-B slot (ShmExchange(slot_bytes=...))")
         # every rank's buffer end, once: a chain that stops short of its shard's stop inside a buffer
         # that does not reach the file's end is a HaloError, and every rank must decide it alike
         # (the others would otherwise wait in their next collective for the rank that raised)
@@ -617,3 +623,37 @@ class DeviceShardedParse:
     def rows(self):
         m = self.metas[self.rank]
         return self.ws.flow_rows(m.n_flows if self.live[self.rank] else 0)
+
+
+def supervise_ranks(target, rank_args, poll_s=0.2, grace_s=10.0):
+    """Start one spawned process per rank (`target(*rank_args[r])`), wait for all of them, and end
+    the others as soon as one exits with a non-zero code: a rank that failed must not leave the rest
+    waiting in a collective (or in a shared-memory exchange) for it.  Returns the exit codes, a
+    terminated rank's as the negative signal number."""
+    import multiprocessing as mp
+    import time
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of the parent's state is inherited
+    procs = [ctx.Process(target=target, args=tuple(a)) for a in rank_args]
+    for p in procs:
+        p.start()
+    try:
+        while any(p.exitcode is None for p in procs):
+            if any(p.exitcode not in (None, 0) for p in procs):
+                for p in procs:
+                    if p.exitcode is None:
+                        p.terminate()
+                t0 = time.monotonic()
+                for p in procs:
+                    p.join(max(0.1, grace_s - (time.monotonic() - t0)))
+                for p in procs:
+                    if p.exitcode is None:
+                        p.kill()
+                        p.join()
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.exitcode is None:
+                p.kill()
+                p.join()
+    return [p.exitcode for p in procs]

@@ -7,6 +7,7 @@ import pytest
 import torch
 
 import _oracle
+import net_parser_rs as npr
 from net_parser_rs import _abi, device, parallel, synth
 
 pytestmark = pytest.mark.gpu
@@ -83,3 +84,43 @@ def test_sharded_device_chain_end():
     _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
     assert r_tot == 9_000 and f_tot == len(flows)
     assert parallel.merge_flows(results, live)[0].tobytes() == flows.tobytes()
+
+
+@pytest.mark.parametrize("lanes", [2, 256])
+@pytest.mark.parametrize("corpus", ["quirk", "c3", "adversarial"])
+def test_shard_buffers_sparse_forced(corpus, lanes):
+    """npr_dev_parse_extract_shard (each shard its own buffer of file bytes [base, end), base > 0,
+    a speculated first record, the speculation context from the host) through the sparse record
+    walk forced on (NPR_OPT_SPARSE 2: lanes sized from the density; 256: 256-B lanes, most of them
+    speculating inside payloads), merged and compared with the serial oracle."""
+    blob = {"quirk": lambda: synth.quirk_corpus(5_000, seed=45),
+            "c3": lambda: synth.variable_mix(6_000),
+            "adversarial": lambda: synth.quirk_corpus(3_000, seed=46, fake_every=3, zero_every=7,
+                                                      jumbo_every=150)}[corpus]()
+    hdr, recs, cons, flows, v6 = reference(blob)
+    host = np.frombuffer(blob, dtype=np.uint8)
+    world, halo = 3, 1 << 17
+    bounds = parallel.shard_bounds(24, len(blob), world)
+    locals_ = []
+    for g, (lo, hi) in enumerate(bounds):
+        base = 0 if g == 0 else lo - lo % 16
+        end = min(len(blob), hi + halo)
+        ws = device.Workspace(record_cap=1, flow_cap=len(recs) + 1, records=False, offsets=False, status=False,
+                              flows=True, flows_v6=True)
+        locals_.append(parallel.shard_local(ws, to_dev(np.ascontiguousarray(host[base:end]).tobytes()), base,
+                                            len(blob), endianness=hdr.endianness, usec_magic=True,
+                                            ts_ref=1_600_000_000, to_host=True))
+    ctx = npr.context(0)  # every Workspace of this thread shares it
+    mode = 2 if lanes == 2 else lanes
+    ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SPARSE, mode))
+    try:
+        results, live, rounds = parallel.parse_sharded_inprocess(locals_, 24, len(blob), world, bounds=bounds)
+        assert ctx.lib.npr_ctx_last_pass(ctx.handle) == _abi.PASS_SPARSE
+    finally:
+        ctx.check(ctx.lib.npr_ctx_set_option(ctx.handle, _abi.OPT_SPARSE, 0))
+    _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
+    assert r_tot == len(recs) and f_tot == len(flows)
+    merged, merged6 = parallel.merge_flows(results, live)
+    assert merged.tobytes() == flows.tobytes()
+    m = (flows["kind"] & _abi.KIND_IPV6) != 0
+    assert merged6[m].tobytes() == v6[m].tobytes()

@@ -238,6 +238,54 @@ def test_corrupt_incl_mid_file_stops_chain(light):
     assert sm.n_records == 12_345
 
 
+def lattice_breaker(kind, n=40_000):
+    """C2-shaped 80-B records with a few records that keep every later record on the 80-B lattice
+    but move its flow index, so that the resident pass's lattice rows (kFlagLattice) of every later
+    range land on wrong rows and must be rewritten exactly: `notok` an unknown EtherType (a non-Ok
+    flow), `double` one 160-B Ok record (a record less), `pair` a 40-B non-Ok + a 120-B Ok record in
+    place of two; `early` breaks the first wave's range, `many` all three kinds at several places."""
+    b = bytearray(synth.fixed64(n))
+    rec = lambda k: 24 + 80 * k
+
+    def notok(k):
+        b[rec(k) + 16 + 12: rec(k) + 16 + 14] = b"\x99\x99"
+
+    def double(k):
+        struct.pack_into("<II", b, rec(k) + 8, 144, 144)
+        b[rec(k + 1): rec(k + 2)] = bytes(80)  # the trailer of the 144-B frame (IPv4 total_length 50)
+
+    def pair(k):
+        frame = bytes(b[rec(k) + 16: rec(k) + 80])
+        struct.pack_into("<II", b, rec(k) + 8, 24, 24)  # 24-B frame: IPv4 incomplete
+        q = rec(k) + 40
+        ts = bytes(b[rec(k): rec(k) + 8])
+        b[q: q + 8] = ts
+        struct.pack_into("<II", b, q + 8, 104, 104)
+        b[q + 16: q + 120] = frame + bytes(40)
+
+    if kind == "notok":
+        notok(n // 2)
+    elif kind == "double":
+        double(n // 3)
+    elif kind == "pair":
+        pair(n // 2 + 7)
+    elif kind == "early":
+        notok(3)
+    elif kind == "many":
+        for k in (5, 1_000, 9_001):
+            notok(k)
+        double(15_000)
+        pair(22_222)
+        double(n - 100)
+    return bytes(b)
+
+
+@LIGHT
+@pytest.mark.parametrize("kind", ["notok", "double", "pair", "early", "many"])
+def test_lattice_breakers(kind, light):
+    check_parity(lattice_breaker(kind), light=light)
+
+
 @LIGHT
 def test_empty_and_header_only(light):
     check_parity(synth.global_header(), light=light)                           # 0 records, rem empty
@@ -384,9 +432,10 @@ CHUNKS = pytest.mark.parametrize("chunk", [1000, 4096, 40_000, 333_333])
 
 
 @CHUNKS
-@pytest.mark.parametrize("corpus", ["c2", "c3", "quirk", "adversarial", "jumbo", "v6"])
+@pytest.mark.parametrize("corpus", ["c2", "c3", "quirk", "adversarial", "jumbo", "v6", "lattice"])
 def test_chunked_matches_serial(corpus, chunk):
     blob = {"c2": lambda: synth.fixed64(30_000),
+            "lattice": lambda: lattice_breaker("many"),
             "c3": lambda: synth.variable_mix(8_000),
             "quirk": lambda: synth.quirk_corpus(6_000, seed=52),
             "adversarial": lambda: synth.quirk_corpus(3_000, seed=53, fake_every=3, zero_every=7, jumbo_every=150),

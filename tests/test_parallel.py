@@ -496,3 +496,79 @@ def test_shm_exchange_latency_world8():
             break
     else:
         assert res["gloo"] > 5000.0, res  # a quiet machine that still misses 80 us
+
+
+# ---- the bench's N = 8 loop on CPU, and a failing rank --------------------------
+class _FailingWorkspace(OracleShardWorkspace):
+    """An oracle workspace whose `fail_at`-th launch raises (a rank that dies mid-loop)."""
+
+    def __init__(self, flow_cap, spec, fail_at):
+        super().__init__(flow_cap, spec)
+        self.fail_at, self.launches = fail_at, 0
+
+    def launch_shard(self, *a, **k):
+        self.launches += 1
+        if self.launches == self.fail_at:
+            raise RuntimeError("injected rank failure")
+        return super().launch_shard(*a, **k)
+
+
+def _step8_rank_main(rank, world, port, blob, fail_rank, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        hdr, recs, cons, flows, v6 = full_reference(blob, with_v6=True)
+        bounds = parallel.shard_bounds(24, len(blob), world)
+        lo, hi = bounds[rank]
+        base = 0 if rank == 0 else lo - lo % 16
+        end = min(len(blob), hi + (1 << 20))
+        shard = torch.from_numpy(np.frombuffer(blob[base:end], dtype=np.uint8).copy())
+        spec = spec_exact(recs)
+        ws = (_FailingWorkspace(len(recs) + 1, spec, fail_at=5) if rank == fail_rank
+              else OracleShardWorkspace(len(recs) + 1, spec))
+        depth = 8  # bench.run_sharded's loop: eight steps in flight, the oldest four per exchange
+        xchg = parallel.ShmExchange(slot_bytes=depth * 64, timeout_s=300.0)
+        step = parallel.DeviceShardedParse(ws, shard, base, bounds, len(blob), depth=depth, exchange=xchg)
+        metas, live, rounds = step.step()
+        for _ in range(20):
+            step.launch_step()
+            if len(step.pending) == depth:
+                metas, live, r = step.finish_steps(depth // 2)
+                rounds = max(rounds, r)
+        metas, live, r = step.finish_steps(len(step.pending))
+        fl, f6 = step.rows()
+        merged, merged6 = parallel.gather_flow_tables(fl, f6, metas, live)
+        if rank == 0:
+            m = merged.numpy().view(_abi.FLOW_DTYPE)
+            m6 = merged6.numpy().view(_abi.FLOW_V6_DTYPE)
+            q.put((m.tobytes() == flows.tobytes(), v6_rows(m, m6) == v6_rows(flows, v6), max(rounds, r)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world8_depth8_shm_loop():
+    """Eight ranks of the bench's N = 8 step loop (DeviceShardedParse at depth 8 over the node-local
+    shared-memory exchange, oracle workspaces), merged table bit-exact on the root."""
+    blob = synth.quirk_corpus(4_000, seed=37)
+    q = mp.get_context("spawn").Queue()
+    port = _free_port()
+    codes = parallel.supervise_ranks(_step8_rank_main, [(r, 8, port, blob, -1, q) for r in range(8)])
+    assert codes == [0] * 8, codes
+    flows_ok, v6_ok, rounds = q.get(timeout=10)
+    assert flows_ok and v6_ok and rounds == 1
+
+
+def test_gloo_world8_failing_rank_ends_the_others():
+    """Rank 5 dies at its fifth launch, with steps in flight on every rank: the others would wait
+    in the exchange (here up to 300 s); supervise_ranks (bench.spawn_ranks) ends them at once."""
+    import time
+    blob = synth.quirk_corpus(4_000, seed=38)
+    q = mp.get_context("spawn").Queue()
+    port = _free_port()
+    t0 = time.monotonic()
+    codes = parallel.supervise_ranks(_step8_rank_main, [(r, 8, port, blob, 5, q) for r in range(8)])
+    took = time.monotonic() - t0
+    assert codes[5] == 1, codes  # the injected exception
+    assert all(c != 0 for c in codes), codes  # nobody finished the loop without rank 5
+    assert took < 120, took
