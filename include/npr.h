@@ -214,7 +214,8 @@ const char *npr_ctx_last_error(const npr_ctx *ctx);
 npr_status npr_stream_release(npr_ctx *ctx, void *stream);
 /* Diagnostics: per-launch speculation / hand-off counters (off by default; costs atomics).
  * Counters: [0] tiles pass 2 re-walked (pass 1's entry was not the exact one), [1] prefix folds
- * that waited for a mis-speculated tile's exact prefix, [5] tiles with no plausible record
+ * that waited for a mis-speculated tile's exact prefix, [3] sparse-walk scan rounds (resolving
+ * contradicted lane groups), [5] tiles with no plausible record
  * start; the others are reserved (0). */
 npr_status npr_ctx_set_stats(npr_ctx *ctx, int enable);
 npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);

@@ -70,6 +70,7 @@ enum : uint32_t {
   kStatRewalk = 0,     // tiles pass 2 re-walked (pass 1's entry was not the exact one)
   kStatMismWait = 1,   // prefixes that waited for a mis-speculated tile's exact prefix
   kStatFoldSlow = 2,   // pass-1 group folds that took the serial (inconsistent-link) path
+  kStatScanRounds = 3, // sparse scan: resolve rounds (0 when the fast path settles every link)
   kStatNoEntry = 5,    // tiles with no plausible record start
   kStatCount = 8
 };

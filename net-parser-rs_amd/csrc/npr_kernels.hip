@@ -53,7 +53,9 @@ __device__ __forceinline__ uint32_t decode_rec(const ParseParams &kp, const uint
   if (__ballot(valid && st == 0xffu)) {  // uniform test: most tiles never take the general path
     if (valid && st == 0xffu) {
       const uint64_t p = tile_lo + rel;
-      TileReader r{w, (const uint8_t *)w, rel + 16u, kp.buf + p + 16, kp.len - p - 16};
+      // (saturated: a record the walk found lies inside the capture, but a position past it must read
+      // zeros, never wrap to a huge reach -- round 4's faulting timing-only build)
+      TileReader r{w, (const uint8_t *)w, rel + 16u, kp.buf + p + 16, p + 16 <= kp.len ? kp.len - p - 16 : 0ull};
       st = decode<FIELDS>(r, incl, f);
     }
   }

@@ -14,10 +14,10 @@
 //     while this one decodes.  Ok flows go to the lane's slots; each 64-lane group (one wave)
 //     publishes its aggregate under the chain-consistency monoid.
 //   k_sparse_scan  one workgroup scans the group aggregates from the anchor (start, or the previous
-//     link's summary).  Groups whose speculation is contradicted are resolved lane by lane from
-//     their incoming chain position (lanes a record spans are marked passed over, mis-speculated
-//     lanes re-walked exactly) and the scan repeats until every link is exact; then it writes each
-//     group's exact prefix and the summary.
+//     link's summary).  Groups whose speculation is contradicted are resolved from their incoming
+//     chain position (lanes a record spans are marked passed over, mis-speculated lanes re-walked
+//     exactly, all such lanes of all flagged groups at once, to a fixed point) and the scan repeats
+//     until every link is exact; then it writes each group's exact prefix and the summary.
 //   k_sparse_rows  one workgroup per group moves its lanes' slots to their convert_records rows
 //     (destination order: whole-line stores); a lane with more Ok flows than slots walks the rest
 //     again from its first slotless record.
@@ -39,6 +39,7 @@ constexpr int kScanThreads = 256;            // k_sparse_scan: one workgroup (at
                                              // paths spilled to scratch: 37 us for the fast path alone)
 constexpr int kResolvers = 256;              // groups resolved per scan round
 constexpr uint32_t kScanWin = 2048;          // groups staged in LDS at a time by the scan's fast path
+constexpr uint32_t kTasks = 2048;            // lane re-walks queued per resolve pass (more wait for the next pass)
 static_assert(15 + 16 + 17 * 4 + 4 <= kSpWin, "header + decode_fast's 68-B window fit the row at any misalignment");
 
 typedef const __attribute__((address_space(1))) u32x4 *gv4_t;  // global (not flat) loads: vmcnt only
@@ -512,42 +513,6 @@ __global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(4))) v
 // (A tree of composite aggregates is not exact here: a record that spans a composite's first group
 // enters it past its entry, which only the lanes can settle.)
 // =============================================================================================
-// Group w resolved from its incoming chain state x (thread-serial): lanes a record spans are marked
-// passed over (entry = exit = the incoming position: their link is then consistent whatever they
-// speculated), mis-speculated lanes walk again from the incoming position; then the group's
-// aggregate is folded again.
-__device__ void resolve_group(const SparseParams &sp, uint32_t w, Seg s, uint32_t *row, uint32_t &rewalks) {
-  const ParseParams &kp = sp.kp;
-  const uint64_t l0 = (uint64_t)w * 64;
-  const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
-  for (uint32_t j = 0; j < size; ++j) {
-    const uint64_t li = l0 + j, hi = sp_end(sp, (int64_t)li);
-    if (s.exit < sp_end(sp, s.last)) break;  // the chain ended before this lane
-    SparseLane L = sp.lanes[li];
-    if (s.exit >= hi) {  // a record spans the lane
-      if (L.entry != s.exit || L.exit != s.exit || L.cnt || L.ok) sp.lanes[li] = SparseLane{s.exit, s.exit, 0u, 0u, kNone, 0ull, 0ull};
-      s.last = (int64_t)li;
-      continue;
-    }
-    if (L.entry != s.exit) {  // mis-speculated: the exact walk from the incoming position
-      uint32_t cnt = 0;
-      AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
-      const uint64_t ex = lane_walk(kp, row, s.exit, hi, cnt, sink);
-      L = SparseLane{s.exit, ex, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
-      sp.lanes[li] = L;
-      ++rewalks;
-    }
-    s.exit = L.exit;
-    s.cnt += L.cnt;
-    s.ok += L.ok;
-    s.last = (int64_t)li;
-  }
-  Seg a = lane_seg(sp, l0, sp.lanes[l0]);
-  for (uint32_t j = 1; j < size; ++j) a = sp_cat(sp, a, lane_seg(sp, l0 + j, sp.lanes[l0 + j]));
-  put_seg(sp.aggs + (uint64_t)w * kSparseAggWords, a);
-  put_lite(sp, w, a);
-}
-
 __device__ __forceinline__ void fence_agent() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent"); }
 
 // a group's plain link: it continues its predecessor's chain exactly (the predecessor did not end
@@ -632,6 +597,8 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
   __shared__ uint64_t entry0;
   __shared__ Seg E0, TOT;
   __shared__ uint32_t rows[kResolvers * kSpRow];
+  __shared__ uint32_t task[kTasks], ntask, npass;  // the resolve's re-walk tasks: flagged index << 6 | lane
+  __shared__ uint64_t tpos[kTasks];                // ... and each task's exact entry
   const ParseParams &kp = sp.kp;
   const uint32_t tid = threadIdx.x, W = sp.ngroups;
   const uint32_t q = W ? (W + kScanThreads - 1) / kScanThreads : 1u;  // groups per thread
@@ -856,15 +823,91 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
         sm->entry = entry0;
         __hip_atomic_store(sp.ctl, gran(kp.epoch, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (kp.stats && rewalks) atomicAdd(kp.stats + kStatRewalk, rewalks);
+        if (kp.stats) atomicAdd(kp.stats + kStatScanRounds, round + 1);
       }
       return;
     }
-    // (3) resolve the flagged groups (the lowest from its exact incoming state), then scan again
+    // (3) resolve the flagged groups (the lowest from its exact incoming state), then scan again:
+    // the serial rule per group is "walk its lanes in order from the incoming position; a lane a
+    // record spans is passed over (entry = exit = the position), a lane whose speculated entry is
+    // not the position walks again from it".  Here lane-parallel, to a fixed point: each wave takes flagged groups and works out, from a group's
+    // incoming state and its lanes' CURRENT exits, the position entering each lane; lanes a record
+    // spans are set passed over, every lane whose entry differs becomes a re-walk task, and all 256
+    // threads take the tasks.  Repeat until no lane changes: each pass makes at least the first
+    // inconsistent lane of every group exact, so it ends, and its fixed point is the serial rule's.
+    // Round 4's one thread per group walked a group's lanes in turn: 15.3 ms of
+    // the 300-MB adversarial capture's 16.3 (901 re-walks).
     const uint32_t nr = nbad < (uint32_t)kResolvers ? nbad : (uint32_t)kResolvers;
-    if (tid < nr) {
+    {
+      const uint32_t lane = tid & 63u, wv = tid >> 6;
       uint32_t rw = 0;
-      resolve_group(sp, bad[tid], badx[tid], rows + tid * kSpRow, rw);
+      for (uint32_t it = 0; it <= 65u; ++it) {
+        if (tid == 0) {
+          ntask = 0;
+          npass = 0;
+        }
+        __syncthreads();
+        for (uint32_t b = wv; b < nr; b += kScanThreads / 64) {  // (a) the tasks of group bad[b]
+          const uint32_t w = bad[b];
+          const Seg sx = badx[b];
+          const uint64_t l0 = (uint64_t)w * 64;
+          const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
+          const uint64_t li = l0 + lane;
+          const bool in = lane < size;
+          const SparseLane L = in ? sp.lanes[li] : SparseLane{};
+          const uint64_t hi = in ? sp_end(sp, (int64_t)li) : 0ull;
+          uint64_t pos = sx.exit, pred = kNone;
+          int64_t last = sx.last;
+          for (uint32_t j = 0; j < size; ++j) {  // (wave-uniform: readlanes of the lanes' current state)
+            if (pos < sp_end(sp, last)) break;   // the chain ended before lane j
+            if (lane == j) pred = pos;
+            last = (int64_t)(l0 + j);
+            if (pos >= rl64(hi, (int)j)) continue;  // a record spans lane j: the position passes on
+            pos = rl64(L.exit, (int)j);
+          }
+          if (in && pred != kNone) {
+            if (pred >= hi) {  // passed over
+              if (L.entry != pred || L.exit != pred || L.cnt || L.ok) {
+                sp.lanes[li] = SparseLane{pred, pred, 0u, 0u, kNone, 0ull, 0ull};
+                atomicAdd(&npass, 1u);
+              }
+            } else if (L.entry != pred) {  // mis-speculated (or its predecessor moved): walk again
+              const uint32_t k = atomicAdd(&ntask, 1u);
+              if (k < kTasks) {
+                task[k] = (b << 6) | lane;
+                tpos[k] = pred;
+              }
+            }
+          }
+        }
+        fence_agent();
+        __syncthreads();
+        fence_agent();
+        const uint32_t nt = ntask < kTasks ? ntask : kTasks;
+        if (nt == 0 && npass == 0) break;
+        for (uint32_t k = tid; k < nt; k += kScanThreads) {  // (b) every thread re-walks tasks
+          const uint32_t b = task[k] >> 6, j = task[k] & 63u, w = bad[b];
+          const uint64_t li = (uint64_t)w * 64 + j, p = tpos[k];
+          uint32_t cnt = 0;
+          AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
+          const uint64_t ex = lane_walk(kp, rows + tid * kSpRow, p, sp_end(sp, (int64_t)li), cnt, sink);
+          sp.lanes[li] = SparseLane{p, ex, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
+          ++rw;
+        }
+        fence_agent();
+        __syncthreads();
+        fence_agent();
+      }
       if (rw) atomicAdd(&rewalks, rw);
+      if (tid < nr) {  // (c) the resolved groups' aggregates
+        const uint32_t w = bad[tid];
+        const uint64_t l0 = (uint64_t)w * 64;
+        const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
+        Seg a = lane_seg(sp, l0, sp.lanes[l0]);
+        for (uint32_t j = 1; j < size; ++j) a = sp_cat(sp, a, lane_seg(sp, l0 + j, sp.lanes[l0 + j]));
+        put_seg(sp.aggs + (uint64_t)w * kSparseAggWords, a);
+        put_lite(sp, w, a);
+      }
     }
     fence_agent();
     __syncthreads();

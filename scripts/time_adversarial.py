@@ -40,6 +40,7 @@ for name, mode in (("sparse", 0), ("resident", 1)):
     ws.ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
     ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
     out[name] = {"ms_median": round(float(np.median(ts[1:])) * 1e3, 3), "pass": lib.npr_ctx_last_pass(h),
-                 "records": sm.n_records, "flows": sm.n_flows, "rewalks_per_launch": st[0] / 6}
+                 "records": sm.n_records, "flows": sm.n_flows, "rewalks_per_launch": st[0] / 6,
+                 "scan_rounds_per_launch": st[3] / 6}
 ws.ctx.check(lib.npr_ctx_set_option(h, _abi.OPT_SPARSE, 0))
 print(json.dumps(out))
