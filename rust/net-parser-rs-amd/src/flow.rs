@@ -15,7 +15,6 @@ use crate::{check, to_record, with_ctx, PcapRecord};
 use device::Device;
 use errors::Error;
 use std::borrow::Cow;
-use std::mem::MaybeUninit;
 use std::net::{IpAddr, Ipv4Addr, Ipv6Addr};
 
 ///
@@ -132,45 +131,48 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
     let (_, header) = crate::GlobalHeader::parse(input)?;
     let big = header.endianness == nom::Endianness::Big;
     let (rows, rows6, consumed) = with_ctx(|ctx| {
-        // Capacity for the most flows the input can hold (one per 16-B record), NOT zero-filled: the
-        // device writes the n rows right-aligned, so only the pages of the last n rows are ever
-        // touched (the rest of the reservation stays virtual), and those n rows are moved into
-        // exactly sized vectors.  (Round 3 zero-filled both: 4x the input, 40 GB for a 10 GB capture.)
-        let cap = input.len().saturating_sub(24) / 16 + 1;
-        let mut rows: Vec<MaybeUninit<ffi::npr_flow>> = Vec::with_capacity(cap);
-        let mut rows6: Vec<MaybeUninit<ffi::npr_flow_v6>> = Vec::with_capacity(cap);
-        let mut hdr = ffi::npr_global_header::default();
-        let (mut n, mut consumed) = (0usize, 0usize);
-        let st = unsafe {
-            ffi::npr_parse_extract_pipelined(
-                ctx,
-                input.as_ptr(),
-                input.len(),
-                &mut hdr,
-                rows.as_mut_ptr() as *mut ffi::npr_flow,
-                rows6.as_mut_ptr() as *mut ffi::npr_flow_v6,
-                cap,
-                &mut n,
-                &mut consumed,
-                0,
-            )
-        };
-        check(ctx, st)?;
-        let k = n.min(cap);
-        // right-aligned: rows[cap - k .. cap] in convert_records order (a side row only where the
-        // flow is IPv6: the others are taken as zero)
-        let tail: Vec<ffi::npr_flow> = (cap - k..cap).map(|i| unsafe { rows.as_ptr().add(i).read().assume_init() }).collect();
-        let tail6: Vec<ffi::npr_flow_v6> = (cap - k..cap)
-            .zip(tail.iter())
-            .map(|(i, f)| {
-                if f.kind & ffi::NPR_FLOW_KIND_IPV6 != 0 {
-                    unsafe { rows6.as_ptr().add(i).read().assume_init() }
-                } else {
-                    ffi::npr_flow_v6::default()
-                }
-            })
-            .collect();
-        Ok((tail, tail6, consumed))
+        // Rows for one flow per 80-B record (a 64-B frame and its header: the smallest common
+        // record) first; a capture of smaller records makes the call report NPR_ERR_CAPACITY with
+        // its exact flow count, and it runs once more into exactly that many rows.  (Round 4
+        // reserved one row per 16 B of input, uninitialised: 4x the input in virtual memory,
+        // which a strict-overcommit host refuses)
+        let cap_all = input.len().saturating_sub(24) / 16 + 1;
+        let mut cap = (input.len().saturating_sub(24) / 80 + 1).min(cap_all);
+        loop {
+            let mut rows = vec![ffi::npr_flow::default(); cap];
+            let mut rows6 = vec![ffi::npr_flow_v6::default(); cap];
+            let mut hdr = ffi::npr_global_header::default();
+            let (mut n, mut consumed) = (0usize, 0usize);
+            let st = unsafe {
+                ffi::npr_parse_extract_pipelined(
+                    ctx,
+                    input.as_ptr(),
+                    input.len(),
+                    &mut hdr,
+                    rows.as_mut_ptr(),
+                    rows6.as_mut_ptr(),
+                    cap,
+                    &mut n,
+                    &mut consumed,
+                    0,
+                )
+            };
+            if st == ffi::NPR_ERR_CAPACITY && n > cap && n <= cap_all {
+                cap = n;
+                continue;
+            }
+            check(ctx, st)?;
+            // right-aligned: rows[cap - k .. cap] in convert_records order (a side row only where
+            // the flow is IPv6: the others are taken as zero)
+            let k = n.min(cap);
+            let tail: Vec<ffi::npr_flow> = rows[cap - k..cap].to_vec();
+            let tail6: Vec<ffi::npr_flow_v6> = rows6[cap - k..cap]
+                .iter()
+                .zip(tail.iter())
+                .map(|(f6, f)| if f.kind & ffi::NPR_FLOW_KIND_IPV6 != 0 { *f6 } else { ffi::npr_flow_v6::default() })
+                .collect();
+            return Ok((tail, tail6, consumed));
+        }
     })?;
     let rd = |b: &[u8]| {
         let a = [b[0], b[1], b[2], b[3]];

@@ -172,6 +172,13 @@ static void run(npr_ctx *ctx, const char *path) {
             "%s: parse_extract_pipelined (%s buffers): %s", path, pass ? "pageable" : "pinned", npr_ctx_last_error(ctx));
     }
   }
+  /* a table one row short: NPR_ERR_CAPACITY with the exact flow count (the Rust crate's
+     parse_and_convert sizes its rows by this and calls again) */
+  if (onf > 0) {
+    size_t nf5 = 0, c5 = 0;
+    CHECK(npr_parse_extract_pipelined(ctx, in, len, &h, fl, fl6, onf - 1, &nf5, &c5, 0) == NPR_ERR_CAPACITY && nf5 == onf,
+          "%s: parse_extract_pipelined one row short: %zu flows reported (%zu)", path, nf5, onf);
+  }
   npr_host_free(ctx, pin);
   npr_host_free(ctx, pfl);
   npr_host_free(ctx, pfl6);
