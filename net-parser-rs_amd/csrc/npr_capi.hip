@@ -923,12 +923,13 @@ npr_status npr_dev_parse_extract_batch(npr_ctx *c, const npr_batch_item *items, 
 // convert_records over device records: one pass, look-back words in the slot allocation
 static npr_status convert_launch(npr_ctx *c, const void *input, uint64_t len, const npr_record *recs, uint64_t n,
                                  npr_flow *out, npr_flow_v6 *out_v6, uint64_t cap, uint64_t *total, hipStream_t s) {
-  npr_status st = ensure(c, c->slots, std::max<uint64_t>(npr::convert_look_words(n), 1) * 8, true);
+  if (!c->cus) (void)hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, c->device);
+  npr_status st = ensure(c, c->slots, std::max<uint64_t>(npr::convert_look_words(n, c->cus), 1) * 8, true);
   if (st) return st;
   if ((st = next_epoch(c, s))) return st;
   return ordered_launch(c, s, [&] {
     return npr::launch_convert_records((const uint8_t *)input, len, recs, n, (uint32_t *)out, (uint32_t *)out_v6, cap,
-                                       (uint64_t *)c->slots.p, c->epoch, total, kTimeoutTicks, s);
+                                       (uint64_t *)c->slots.p, c->epoch, total, kTimeoutTicks, c->cus, s);
   });
 }
 

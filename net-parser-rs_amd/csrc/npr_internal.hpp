@@ -142,11 +142,12 @@ uint64_t flow_table_bytes(uint64_t n);
 constexpr uint64_t kMaxAggRows = 1ull << 30;  // rows per call: S = 2^31 slots, 32-bit slot indices
 // convert_records in one pass (k_convert_records): rows 0.. = Ok flows in reverse record order,
 // *total = all Ok flows (rows past cap are not written; ~0 when a bounded wait timed out).
-// look: convert_look_words(n) granules whose tags are not `epoch` at launch.
+// look: convert_look_words(n, cus) granules whose tags are not `epoch` at launch; cus = the
+// device's CU count (it sets the records per lane).
 hipError_t launch_convert_records(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
                                   uint32_t *out, uint32_t *out_v6, uint64_t cap, uint64_t *look, uint32_t epoch,
-                                  uint64_t *total, uint64_t timeout_ticks, hipStream_t s);
-uint64_t convert_look_words(uint64_t n);
+                                  uint64_t *total, uint64_t timeout_ticks, int cus, hipStream_t s);
+uint64_t convert_look_words(uint64_t n, int cus);
 
 // ---- the sparse record walk (npr_sparse.hip): flows-only parses of captures of
 // long records.  The range [start, stop) is cut into lane ranges of `span` bytes; each lane

@@ -2189,18 +2189,25 @@ hipError_t launch_vxlan_flows(const uint8_t *buf, uint64_t len, const npr_record
 }
 
 // ---------------------------------------------------------------------------------------------
-// convert_records in ONE pass.  Workgroup j takes the j-th block of kBlock x kCvtPer records FROM
-// THE END of the list, so its Ok flows' reverse-order rows start at the number of Ok flows in the
-// blocks after it: exactly the lower-numbered (earlier dispatched) workgroups.  Each workgroup
-// publishes its count A(j) (an epoch-tagged granule) and sums the counts below it: whole groups of
-// 64 through their sums S(g) (published by each group's top member from its own group's counts),
-// its own group member by member.  No workgroup waits along a chain of look-backs: only for
-// counts, which every workgroup publishes as soon as its records are decoded.
+// convert_records in ONE pass.  One 1024-thread workgroup per CU: workgroup j takes the j-th block
+// of rpb records FROM THE END of the list (launch_convert_records), so its Ok flows' reverse-order rows
+// start at the number of Ok flows in the blocks after it: exactly the lower-numbered (earlier
+// dispatched) workgroups.  A CU's 16 waves share its memory pipeline and finish their block
+// together, so the counts all come in at about the same time.  (With four 256-thread workgroups
+// per CU, the SIMD arbiter's age order made the youngest workgroup of each CU take 1.6x the
+// oldest's time to decode, and every prefix above it waited for it: profiles/r05_convert_stamps.txt.)
+// Each workgroup publishes its count A(j) (an epoch-tagged granule).  Waves 0..3 each read one
+// window of 64 counts at once: the blocks below j in its own group of 64 and in the three groups
+// below that.  Wave 0 adds the sums S(g) of the groups further down; each S(g) is published by the
+// group's top member from its own group's window, never from another look-back.  Up to 256
+// workgroups (1M records) that is ONE round trip, and no workgroup waits along a chain.
 // The flows stay in registers (kCvtPer records per lane) until the start row is known.  The
 // workgroup of the list's first block writes the total (~0 when a bounded wait timed out).
 // ---------------------------------------------------------------------------------------------
-// kCvtPer records per lane; kRows of their payload windows staged (LDS rows) at a time
-constexpr uint32_t kCvtGroup = 64;            // workgroups per group sum
+constexpr uint32_t kCvtBlock = 1024;  // threads per workgroup; its LDS (> 80 KB) keeps it alone on its CU
+constexpr uint32_t kCvtWaves = kCvtBlock / kWave;
+constexpr uint32_t kCvtGroup = 64;    // workgroups per group sum
+constexpr uint32_t kCvtNear = 4;      // groups whose counts are read directly (waves 0..3)
 
 __device__ __forceinline__ uint64_t cvt_wait_sum(const uint64_t *w, int64_t cnt, uint32_t epoch, uint64_t t0,
                                                  uint64_t timeout, bool &ok) {
@@ -2213,7 +2220,7 @@ __device__ __forceinline__ uint64_t cvt_wait_sum(const uint64_t *w, int64_t cnt,
       ok = false;
       return 0;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(8);
     if ((v >> 48) != epoch) v = __hip_atomic_load(w + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   uint64_t x = v & kMask48;
@@ -2222,33 +2229,33 @@ __device__ __forceinline__ uint64_t cvt_wait_sum(const uint64_t *w, int64_t cnt,
 }
 
 template <int kCvtPer, int kRows>
-__global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, uint64_t len,
-                                                            const npr_record *recs, uint64_t n, uint32_t *out,
-                                                            uint32_t *out_v6, uint64_t cap, uint64_t *look,
-                                                            uint32_t epoch, uint64_t *total,
-                                                            uint64_t timeout) {
-  __shared__ uint32_t rows[kRows][kBlock * kRowWords];
-  __shared__ uint32_t wc[kCvtPer][kBlock / kWave];
+__global__ __launch_bounds__(kCvtBlock) void k_convert_records(const uint8_t *buf, uint64_t len,
+                                                               const npr_record *recs, uint64_t n, uint32_t *out,
+                                                               uint32_t *out_v6, uint64_t cap, uint64_t *look,
+                                                               uint32_t epoch, uint64_t *total,
+                                                               uint64_t timeout, uint32_t rpb) {
+  __shared__ uint32_t rows[kRows][kCvtBlock * kRowWords];
+  __shared__ uint32_t wc[kCvtPer][kCvtWaves];
+  __shared__ uint64_t part[kCvtNear];
   __shared__ uint64_t excl_sh;
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t j = blockIdx.x, nb = gridDim.x;
-  constexpr int kCvtRecs = kBlock * kCvtPer;
-  const int64_t lo = (int64_t)n - (int64_t)(j + 1) * kCvtRecs;  // this block: records [lo, lo + kCvtRecs) clipped at 0
+  const int64_t lo = (int64_t)n - (int64_t)(j + 1) * rpb;  // this block: records [lo, lo + rpb) clipped at 0
   uint32_t kd[kCvtPer][7];   // flow words d[0..6] (IPv6: d[0] = the address block's payload offset)
   uint64_t koff[kCvtPer];
   uint32_t okm = 0;
-  // every record row in flight together; then the payload windows, kRows at a time (each lane
-  // stages kRows windows in LDS: kRows = kCvtPer issues all of them at once)
+  // every record row in flight together; then the payload windows, one staged LDS row per lane
   npr_record rc[kCvtPer];
 #pragma unroll
   for (int r = 0; r < kCvtPer; ++r) {
-    const int64_t i = lo + r * kBlock + (int64_t)threadIdx.x;
-    rc[r] = i >= 0 ? load_record(recs, (uint64_t)i) : npr_record{len, 0, 0, 0, 0};  // (past the buffer: no flow)
+    const uint32_t k = (uint32_t)r * kCvtBlock + threadIdx.x;  // the lane's record of round r in the block
+    const int64_t i = lo + (int64_t)k;
+    rc[r] = i >= 0 && k < rpb ? load_record(recs, (uint64_t)i) : npr_record{len, 0, 0, 0, 0};  // (past the buffer: no flow)
   }
   // the payload windows: record r + 1's is loaded into registers while record r (staged in the
   // lane's LDS row) decodes, so one window's latency is in flight behind each decode.  The loads are
-  // unconditional (a record whose window does not lie inside the buffer loads the buffer's first
-  // bytes, unused) so that the compiler counts them and waits for the older one only.
+  // unconditional (a record whose window does not lie inside the buffer loads kZeroWin, unused) so
+  // that the compiler counts them and waits for the older one only.
   static_assert(kRows == 1, "one staged row per lane (the next window waits in registers)");
   typedef const __attribute__((address_space(1))) u32x4 *gwin_t;  // global loads (not flat: counted by vmcnt only)
   auto win_load = [&](const npr_record &c, bool f, RowWin &W) {
@@ -2288,61 +2295,63 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
 #pragma unroll
   for (int r = 0; r < kCvtPer; ++r)
 #pragma unroll
-    for (int w = 0; w < kBlock / kWave; ++w) cnt += wc[r][w];
-  if (wave == 0) {
-    const uint64_t tag = (uint64_t)epoch << 48;
-    const uint64_t g = j / kCvtGroup, g0 = g * kCvtGroup;
-    uint64_t *A = look, *S = look + nb;
+    for (uint32_t w = 0; w < kCvtWaves; ++w) cnt += wc[r][w];
+  const uint64_t tag = (uint64_t)epoch << 48;
+  uint64_t *A = look, *S = look + nb;
+  uint64_t *abortw = look + nb + (nb + kCvtGroup - 1) / kCvtGroup;
+  if (wave < kCvtNear) {
+    // start row = sum S(groups below gl - 3) + every count of groups gl - 3 .. gl below j
+    const uint64_t gl = j / kCvtGroup;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     bool ok = true;
-    if (lane == 0) __hip_atomic_store(A + j, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // start row = sum S(groups below g) + sum A(this group's lower members).  S(g) is published by
-    // the group's top member (j = g0 + 63) once its own window is in: it depends on group g's counts
-    // only, never on another look-back.  One round trip in the common case: the (up to) 64 group
-    // sums just below g and this group's lower counts, loaded at once.
-    const uint64_t sbase = g > 64 ? g - 64 : 0;
-    const bool s_in = sbase + lane < g, a_in = g0 + lane < j;
-    uint64_t sv = s_in ? __hip_atomic_load(S + sbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
-    uint64_t av = a_in ? __hip_atomic_load(A + g0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
-    const bool top = j == g0 + kCvtGroup - 1;
-    bool s_done = !top;
-    for (;;) {
-      const bool s_miss = s_in && (sv >> 48) != epoch, a_miss = a_in && (av >> 48) != epoch;
-      if (!s_done && !__ballot(a_miss)) {  // the top member: S(g) as soon as its group's counts are in
-        uint64_t y = a_in ? av & kMask48 : 0ull;
-        for (int o = 32; o > 0; o >>= 1) y += __shfl_xor(y, o);
-        if (lane == 0) __hip_atomic_store(S + g, tag | (y + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_done = true;
+    uint64_t sum = 0;
+    if (wave == 0 && lane == 0) __hip_atomic_store(A + j, tag | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave <= gl) {  // (uniform) group gl - wave exists
+      const uint64_t g = gl - wave, g0 = g * kCvtGroup;
+      const bool a_in = g0 + lane < j;
+      uint64_t av = a_in ? __hip_atomic_load(A + g0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
+      for (;;) {
+        const bool a_miss = a_in && (av >> 48) != epoch;
+        if (!__ballot(a_miss)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+          ok = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+        if (a_miss) av = __hip_atomic_load(A + g0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (!__ballot(s_miss || a_miss)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
-        ok = false;
-        break;
+      uint64_t y = a_in ? av & kMask48 : 0ull;
+      for (int o = 32; o > 0; o >>= 1) y += __shfl_xor(y, o);
+      sum = y;
+      // the group's top member publishes S(g) as soon as its own group's counts are in
+      if (ok && wave == 0 && j == g0 + kCvtGroup - 1 && lane == 0)
+        __hip_atomic_store(S + g, tag | (y + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wave == 0 && gl >= kCvtNear) {  // groups 0 .. gl - 4 through their sums (lists > 1M records)
+        const uint64_t nfar = gl - kCvtNear + 1;
+        for (uint64_t k = 0; k < nfar && ok; k += 64)
+          sum += cvt_wait_sum(S + k, (int64_t)(nfar - k < 64 ? nfar - k : 64), epoch, t0, timeout, ok);
       }
-      __builtin_amdgcn_s_sleep(8);
-      if (s_miss) sv = __hip_atomic_load(S + sbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (a_miss) av = __hip_atomic_load(A + g0 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (lane == 0) part[wave] = ok ? sum : ~0ull;
+  }
+  __syncthreads();
+  // a workgroup whose wait timed out writes no rows: it raises the launch's abort granule, and the
+  // block holding record 0 (which depends, through the group sums, on every count any other block
+  // waits for, so it finishes its own wait after any such timeout) reports ~0 when it is raised
+  if (threadIdx.x == 0) {
+    bool ok = true;
     uint64_t acc = 0;
-    if (ok) {
-      uint64_t x = (s_in ? sv & kMask48 : 0ull) + (a_in ? av & kMask48 : 0ull);
-      for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-      acc = x;
-      for (uint64_t k = 0; k < sbase && ok; k += 64)  // groups more than 64 below (lists > 64 x 64 blocks)
-        acc += cvt_wait_sum(S + k, (int64_t)(sbase - k < 64 ? sbase - k : 64), epoch, t0, timeout, ok);
+#pragma unroll
+    for (uint32_t w = 0; w < kCvtNear; ++w) {
+      ok = ok && part[w] != ~0ull;
+      acc += part[w];
     }
-    // a workgroup whose wait timed out writes no rows: it raises the launch's abort granule, and the
-    // block holding record 0 (which depends, through the group sums, on every count any other block
-    // waits for, so it finishes its own wait after any such timeout) reports ~0 when it is raised
-    uint64_t *abortw = look + nb + (nb + kCvtGroup - 1) / kCvtGroup;
-    if (!ok && lane == 0) __hip_atomic_store(abortw, tag | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 0) {
-      excl_sh = ok ? acc : ~0ull;
-      if (j == nb - 1) {  // the block holding record 0
-        const bool aborted =
-            ok && (__hip_atomic_fetch_add(abortw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 48) == epoch;
-        *total = ok && !aborted ? acc + cnt : ~0ull;
-      }
+    if (!ok) __hip_atomic_store(abortw, tag | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    excl_sh = ok ? acc : ~0ull;
+    if (j == nb - 1) {  // the block holding record 0
+      const bool aborted =
+          ok && (__hip_atomic_fetch_add(abortw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> 48) == epoch;
+      *total = ok && !aborted ? acc + cnt : ~0ull;
     }
   }
   __syncthreads();
@@ -2351,7 +2360,7 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
   // rows: excl + the Ok flows of this block at higher record indices (later r, higher wave, higher
   // lane).  Each round's rows are one contiguous block: staged in LDS, stored as whole lines (one
   // 32-B row per lane at a 32-B stride writes at a fraction of the rate: store_pattern.hip)
-  __shared__ __attribute__((aligned(16))) uint4 cstg[kBlock * 2 + 8];  // stg_slot<2 kBlock> layout
+  __shared__ __attribute__((aligned(16))) uint4 cstg[kCvtBlock * 2 + 8];  // stg_slot<2 kCvtBlock> layout
   uint64_t after = excl;
 #pragma unroll
   for (int r = kCvtPer - 1; r >= 0; --r) {
@@ -2359,23 +2368,23 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
     const uint64_t bal = __ballot(ok);
     uint32_t above = 0, rc = 0;
 #pragma unroll
-    for (int w = 0; w < kBlock / kWave; ++w) {
-      above += (uint32_t)w > wave ? wc[r][w] : 0u;
+    for (uint32_t w = 0; w < kCvtWaves; ++w) {
+      above += w > wave ? wc[r][w] : 0u;
       rc += wc[r][w];
     }
     const uint32_t lr = above + (uint32_t)__builtin_popcountll(bal & ~((2ull << lane) - 1ull));
     __syncthreads();  // the previous round's chunks are read
     if (ok) {
       const bool is6 = (kd[r][6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-      cstg[stg_slot<2 * kBlock>(2 * lr)] = make_uint4(is6 ? 0u : kd[r][0], kd[r][1], kd[r][2], kd[r][3]);
-      cstg[stg_slot<2 * kBlock>(2 * lr + 1)] = make_uint4(kd[r][4], kd[r][5], kd[r][6] | ((uint32_t)(koff[r] & 0xffu) << 24), (uint32_t)(koff[r] >> 8));
+      cstg[stg_slot<2 * kCvtBlock>(2 * lr)] = make_uint4(is6 ? 0u : kd[r][0], kd[r][1], kd[r][2], kd[r][3]);
+      cstg[stg_slot<2 * kCvtBlock>(2 * lr + 1)] = make_uint4(kd[r][4], kd[r][5], kd[r][6] | ((uint32_t)(koff[r] & 0xffu) << 24), (uint32_t)(koff[r] >> 8));
     }
     __syncthreads();
     uint4 *blk = reinterpret_cast<uint4 *>(out + after * 8);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const uint32_t c = threadIdx.x + (uint32_t)h * kBlock;
-      if (c < 2u * rc && after + c / 2u < cap) st_nt16(blk + c, cstg + stg_slot<2 * kBlock>(c));  // (30.3 -> 28.6 us per 1M)
+      const uint32_t c = threadIdx.x + (uint32_t)h * kCvtBlock;
+      if (c < 2u * rc && after + c / 2u < cap) st_nt16(blk + c, cstg + stg_slot<2 * kCvtBlock>(c));
     }
     if (ok) {
       const uint64_t rw = after + lr;
@@ -2397,29 +2406,43 @@ __global__ __launch_bounds__(kBlock) void k_convert_records(const uint8_t *buf, 
   }
 }
 
-// 4 records per lane, one staged window at a time (the next one prefetched into registers): measured
-// best on C2 (37.6 us per 1M records before the row staging and the prefetch, 28.5 us with them;
-// 1 / 2 records per lane 53.7 / 41.9 us, 4 with two windows staged at once 47.7 us: LDS-bound
-// occupancy; a persistent kernel writing each round's rows while the next round loads, 29.9 us:
-// profiles/r03_convert_experiment_ab.json)
-constexpr int kCvtPer = 4, kCvtRows = 1;
-uint64_t convert_blocks(uint64_t n) {
-  const uint64_t r = (uint64_t)kBlock * kCvtPer;
-  return (n + r - 1) / r;
+// The list is dealt to one workgroup per CU in blocks of rpb = ceil(n / CUs) records, rounded up to
+// 256 (at least one per lane, at most kCvtMaxPer per lane: longer lists take several generations
+// of workgroups), so every CU gets the same share; a lane takes ceil(rpb / 1024) records, one staged
+// window at a time, the next one prefetched into registers.  The rounding keeps a block's row runs
+// on 8-KB boundaries when every record is Ok: 1M records in blocks of 3907 (256 workgroups, row runs
+// splitting lines at every block edge) took 32.1 us, in blocks of 4096 (245 workgroups) 30.6 us
+// (profiles/r05_convert_rework.txt).
+constexpr int kCvtRows = 1, kCvtMaxPer = 4;
+struct CvtShape {
+  uint32_t rpb;  // records per block
+  int per;       // records per lane (1 .. kCvtMaxPer)
+  uint64_t nb;   // blocks
+};
+static CvtShape convert_shape(uint64_t n, int cus) {
+  const uint64_t c = cus > 0 ? (uint64_t)cus : 256u;
+  uint64_t rpb = (n + c - 1) / c;
+  rpb = (rpb + 255) / 256 * 256;
+  rpb = rpb < kCvtBlock ? kCvtBlock : rpb > (uint64_t)kCvtMaxPer * kCvtBlock ? (uint64_t)kCvtMaxPer * kCvtBlock : rpb;
+  return {(uint32_t)rpb, (int)((rpb + kCvtBlock - 1) / kCvtBlock), n ? (n + rpb - 1) / rpb : 0};
 }
-uint64_t convert_look_words(uint64_t n) {  // counts, group sums, the abort granule
-  const uint64_t nb = convert_blocks(n);
+uint64_t convert_look_words(uint64_t n, int cus) {  // counts, group sums, the abort granule
+  const uint64_t nb = convert_shape(n, cus).nb;
   return nb + (nb + kCvtGroup - 1) / kCvtGroup + 1;
 }
 
 hipError_t launch_convert_records(const uint8_t *buf, uint64_t len, const npr_record *recs, uint64_t n,
-                                  uint32_t *out, uint32_t *out_v6, uint64_t cap, uint64_t *look, uint32_t epoch, uint64_t *total, uint64_t timeout_ticks, hipStream_t s) {
-  const uint64_t nb = convert_blocks(n);
-  if (nb == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
-  if (nb > 0x7fffffffull) return hipErrorInvalidValue;
-  auto k = k_convert_records<kCvtPer, kCvtRows>;
-  hipLaunchKernelGGL(k, dim3((uint32_t)nb), dim3(kBlock), 0, s, buf, len, recs, n, out, out_v6, cap,
-                     look, epoch, total, timeout_ticks);
+                                  uint32_t *out, uint32_t *out_v6, uint64_t cap, uint64_t *look, uint32_t epoch,
+                                  uint64_t *total, uint64_t timeout_ticks, int cus, hipStream_t s) {
+  const CvtShape sh = convert_shape(n, cus);
+  if (sh.nb == 0) return hipMemsetAsync(total, 0, sizeof(uint64_t), s);
+  if (sh.nb > 0x7fffffffull) return hipErrorInvalidValue;
+  auto k = sh.per == 1 ? k_convert_records<1, kCvtRows>
+           : sh.per == 2 ? k_convert_records<2, kCvtRows>
+           : sh.per == 3 ? k_convert_records<3, kCvtRows>
+                         : k_convert_records<4, kCvtRows>;
+  hipLaunchKernelGGL(k, dim3((uint32_t)sh.nb), dim3(kCvtBlock), 0, s, buf, len, recs, n, out, out_v6, cap,
+                     look, epoch, total, timeout_ticks, sh.rpb);
   return hipGetLastError();
 }
 

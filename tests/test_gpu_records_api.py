@@ -83,7 +83,10 @@ def test_dev_per_record_matches_oracle(name, variant):
     assert check_convert(blob, recs) > 0 or name == "adversarial"
 
 
-@pytest.mark.parametrize("n", [0, 1, 255, 256, 257, 511, 513, 64 * 256 + 3])
+# block shapes on 256 CUs (launch_convert_records): one record per lane up to 256 x 1024, then 2, 3
+# and 4 per lane with ragged last rounds, then several generations of 4096-record blocks
+@pytest.mark.parametrize("n", [0, 1, 255, 1023, 1024, 1025, 64 * 256 + 3, 256 * 1024, 256 * 1024 + 1, 600_000,
+                               256 * 4096, 256 * 4096 + 1])
 def test_dev_convert_block_edges(n):
     blob = synth.fixed64(max(n, 1))
     recs = records_of(blob)[:n]
@@ -125,10 +128,19 @@ def test_dev_convert_c2_full_size():
     check_dense(blob, recs)
 
 
-def test_dev_convert_beyond_64_groups():
-    """A list of more than 64 x 64 blocks of 1024 records (4.3M frames): the start rows of the upper
-    blocks fold group sums more than 64 groups below them, and a ragged last block."""
+def test_dev_convert_far_groups():
+    """4.3M frames: 1,052 blocks of 4096 records, so the upper blocks take the groups more than
+    three below their own through the group sums, and a ragged last block."""
     n = 64 * 64 * 1024 + 111_111
+    blob = synth.fixed64(n)
+    recs = records_of(blob)
+    assert check_convert(blob, recs) == n
+
+
+def test_dev_convert_beyond_64_group_sums():
+    """17.8M frames (1.4 GB): 4,356 blocks, so the top blocks fold more than 64 group sums (two
+    windows of sums) below their near groups."""
+    n = 68 * 64 * 4096 + 12_345
     blob = synth.fixed64(n)
     recs = records_of(blob)
     assert check_convert(blob, recs) == n
