@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define NPR_ABI_VERSION 4
+#define NPR_ABI_VERSION 5
 
 /* ---- status of an API call ------------------------------------------------------------ */
 typedef enum npr_status {
@@ -291,6 +291,120 @@ npr_status npr_global_header_parse(const uint8_t *input, size_t len, npr_global_
 /* PcapRecord::parse (src/record.rs:102-121). *consumed = 16 + actual_length. */
 npr_status npr_record_parse(const uint8_t *input, size_t len, npr_endianness endianness,
                             npr_record *out, size_t *consumed);
+
+/* ---- host-side per-layer header objects (the reference's public layer parsers) ------------------
+ * Each parses ONE header object from `input` as its reference function does (the nom chain step by
+ * step, with the reference's release-build wrapping arithmetic).  No device work: these are the
+ * object API for callers that inspect frames; the flows of whole captures come from the device.
+ * Byte ranges of `input` (the reference's borrowed slices) are {offset, length} pairs.  Returns
+ *   NPR_OK: `*out` filled, *consumed = the bytes the parser used (its remainder is input[*consumed..]);
+ *   NPR_INCOMPLETE: *detail = nom's Needed::Size of the failing primitive (be_u16: 2, take!(k): k);
+ *   NPR_FAILURE: a map_opt! / map_res! failed; *detail = start | end << 32, the offsets in `input`
+ *     of the failing primitive's input and of its end (nom's Context::Code input slice);
+ *   NPR_CUSTOM: the IP version check failed; *detail = the version nibble.
+ * `consumed` and `detail` may be NULL. */
+/* VlanTag (src/layer2/ethernet.rs:85-98): prio and dei are the reference's `(total & 0x7000) as u8`
+ * and `(total & 0x8000) as u8`, i.e. always 0. */
+typedef struct npr_vlan_tag {
+  uint16_t vlan_type;  /* VlanTypeId::value(): 0x8100 or 0x88A8 */
+  uint16_t vlan_value; /* the tag's 16 bits */
+  uint8_t prio;
+  uint8_t dei;
+  uint16_t id;         /* vlan_value & 0x0FFF */
+} npr_vlan_tag;
+/* Ethernet (src/layer2/ethernet.rs:100-107) */
+typedef struct npr_ethernet {
+  uint8_t dst_mac[6];
+  uint8_t src_mac[6];
+  uint16_t ether_type; /* EthernetTypeId::value(): an 802.3 length (<= 1500) or 0x0800 / 0x86DD / 0x0806 / 0x88CC */
+  uint16_t reserved;
+  uint32_t n_vlans;    /* the frame's VLAN tags, outermost first; the first min(n_vlans, vlan_cap) go to `vlans` */
+  uint64_t payload_offset, payload_length;
+} npr_ethernet;
+/* Ethernet::parse (src/layer2/ethernet.rs:204-216).  More tags than vlan_cap: NPR_ERR_CAPACITY with
+ * the exact n_vlans (the other fields filled). */
+npr_status npr_ethernet_parse(const uint8_t *input, size_t len, npr_ethernet *out, npr_vlan_tag *vlans,
+                              size_t vlan_cap, size_t *consumed, uint64_t *detail);
+/* IPv4 (src/layer3/ipv4.rs:14-29).  options / padding: length 0 = None (the reference's cond! takes
+ * them only when they are non-empty). */
+typedef struct npr_ipv4 {
+  uint8_t version_and_length;
+  uint8_t tos;
+  uint16_t raw_length;
+  uint16_t id;
+  uint16_t flags;
+  uint8_t ttl;
+  uint8_t protocol;    /* InternetProtocolId::value() */
+  uint16_t checksum;
+  uint8_t src_ip[4];
+  uint8_t dst_ip[4];
+  uint64_t payload_offset, payload_length;
+  uint64_t options_offset, options_length;
+  uint64_t padding_offset, padding_length;
+} npr_ipv4;
+/* IPv4::parse (src/layer3/ipv4.rs:148-160) + parse_ipv4 (:76-146) */
+npr_status npr_ipv4_parse(const uint8_t *input, size_t len, npr_ipv4 *out, size_t *consumed, uint64_t *detail);
+/* IPv6 (src/layer3/ipv6.rs:10-16) */
+typedef struct npr_ipv6 {
+  uint8_t dst_ip[16];
+  uint8_t src_ip[16];
+  uint8_t protocol;    /* the first next header that has no next option (InternetProtocolId::value()) */
+  uint8_t reserved[7];
+  uint64_t payload_offset, payload_length;
+} npr_ipv6;
+/* IPv6::parse (src/layer3/ipv6.rs:87-99): one byte per "extension" header (quirk Q11). */
+npr_status npr_ipv6_parse(const uint8_t *input, size_t len, npr_ipv6 *out, size_t *consumed, uint64_t *detail);
+/* Arp (src/layer3/arp.rs:7-14) */
+typedef struct npr_arp {
+  uint8_t sender_ip[4];
+  uint8_t sender_mac[6];
+  uint8_t target_ip[4];
+  uint8_t target_mac[6];
+  uint16_t operation;
+} npr_arp;
+/* Arp::parse (src/layer3/arp.rs:54-76) */
+npr_status npr_arp_parse(const uint8_t *input, size_t len, npr_arp *out, size_t *consumed, uint64_t *detail);
+/* Tcp (src/layer4/tcp.rs:11-30) with its HeaderLengthAndFlags */
+typedef struct npr_tcp {
+  uint16_t src_port;
+  uint16_t dst_port;
+  uint32_t sequence_number;
+  uint32_t acknowledgement_number;
+  uint16_t header_length_and_flags; /* HeaderLengthAndFlags::inner */
+  uint16_t flags;                   /* inner & 0x01FF */
+  uint32_t header_length;           /* (inner >> 12) * 4, in [20, 60] */
+  uint16_t window;
+  uint16_t check;
+  uint16_t urgent;
+  uint16_t reserved;
+  uint64_t options_offset, options_length;
+  uint64_t payload_offset, payload_length;
+} npr_tcp;
+/* Tcp::parse (src/layer4/tcp.rs:59-101) */
+npr_status npr_tcp_parse(const uint8_t *input, size_t len, npr_tcp *out, size_t *consumed, uint64_t *detail);
+/* Udp (src/layer4/udp.rs:10-16) */
+typedef struct npr_udp {
+  uint16_t src_port;
+  uint16_t dst_port;
+  uint16_t checksum;
+  uint16_t reserved;
+  uint64_t payload_offset, payload_length;
+} npr_udp;
+/* Udp::parse (src/layer4/udp.rs:33-50): the payload is take!(length - 8) with the reference's usize
+ * arithmetic, so a length field below 8 asks for ~2^64 bytes (NPR_INCOMPLETE, *detail = that size). */
+npr_status npr_udp_parse(const uint8_t *input, size_t len, npr_udp *out, size_t *consumed, uint64_t *detail);
+/* Vxlan (src/layer4/vxlan.rs:7-14) */
+typedef struct npr_vxlan {
+  uint16_t flags;
+  uint16_t group_policy_id;
+  uint32_t raw_network_identifier;
+  uint32_t network_identifier;      /* raw >> 8 */
+  uint32_t reserved;
+  uint64_t payload_offset, payload_length;
+} npr_vxlan;
+/* Vxlan::parse (src/layer4/vxlan.rs:31-48): u16! u16! u32! in `endianness`, then the rest. */
+npr_status npr_vxlan_parse(const uint8_t *input, size_t len, npr_endianness endianness, npr_vxlan *out,
+                           size_t *consumed, uint64_t *detail);
 
 /* ---- host-memory entry points (stage to HBM, run the device path, copy back) ------------- */
 /* PcapRecords::parse (src/record.rs:21-54): records from byte 0, stop at the first Incomplete.

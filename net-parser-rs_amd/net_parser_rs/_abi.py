@@ -103,7 +103,65 @@ class SummaryC(ctypes.Structure):
                 ("epoch", ctypes.c_uint32), ("entry", ctypes.c_uint64)]
 
 
+# ---- host-side per-layer header objects (npr.h "host-side per-layer header objects") -------------
+_u64 = ctypes.c_uint64
+
+
+class VlanTagC(ctypes.Structure):
+    _fields_ = [("vlan_type", ctypes.c_uint16), ("vlan_value", ctypes.c_uint16), ("prio", ctypes.c_uint8),
+                ("dei", ctypes.c_uint8), ("id", ctypes.c_uint16)]
+
+
+class EthernetC(ctypes.Structure):
+    _fields_ = [("dst_mac", ctypes.c_uint8 * 6), ("src_mac", ctypes.c_uint8 * 6), ("ether_type", ctypes.c_uint16),
+                ("reserved", ctypes.c_uint16), ("n_vlans", ctypes.c_uint32), ("payload_offset", _u64),
+                ("payload_length", _u64)]
+
+
+class IPv4C(ctypes.Structure):
+    _fields_ = [("version_and_length", ctypes.c_uint8), ("tos", ctypes.c_uint8), ("raw_length", ctypes.c_uint16),
+                ("id", ctypes.c_uint16), ("flags", ctypes.c_uint16), ("ttl", ctypes.c_uint8),
+                ("protocol", ctypes.c_uint8), ("checksum", ctypes.c_uint16), ("src_ip", ctypes.c_uint8 * 4),
+                ("dst_ip", ctypes.c_uint8 * 4), ("payload_offset", _u64), ("payload_length", _u64),
+                ("options_offset", _u64), ("options_length", _u64), ("padding_offset", _u64),
+                ("padding_length", _u64)]
+
+
+class IPv6C(ctypes.Structure):
+    _fields_ = [("dst_ip", ctypes.c_uint8 * 16), ("src_ip", ctypes.c_uint8 * 16), ("protocol", ctypes.c_uint8),
+                ("reserved", ctypes.c_uint8 * 7), ("payload_offset", _u64), ("payload_length", _u64)]
+
+
+class ArpC(ctypes.Structure):
+    _fields_ = [("sender_ip", ctypes.c_uint8 * 4), ("sender_mac", ctypes.c_uint8 * 6),
+                ("target_ip", ctypes.c_uint8 * 4), ("target_mac", ctypes.c_uint8 * 6),
+                ("operation", ctypes.c_uint16)]
+
+
+class TcpC(ctypes.Structure):
+    _fields_ = [("src_port", ctypes.c_uint16), ("dst_port", ctypes.c_uint16), ("sequence_number", ctypes.c_uint32),
+                ("acknowledgement_number", ctypes.c_uint32), ("header_length_and_flags", ctypes.c_uint16),
+                ("flags", ctypes.c_uint16), ("header_length", ctypes.c_uint32), ("window", ctypes.c_uint16),
+                ("check", ctypes.c_uint16), ("urgent", ctypes.c_uint16), ("reserved", ctypes.c_uint16),
+                ("options_offset", _u64), ("options_length", _u64), ("payload_offset", _u64),
+                ("payload_length", _u64)]
+
+
+class UdpC(ctypes.Structure):
+    _fields_ = [("src_port", ctypes.c_uint16), ("dst_port", ctypes.c_uint16), ("checksum", ctypes.c_uint16),
+                ("reserved", ctypes.c_uint16), ("payload_offset", _u64), ("payload_length", _u64)]
+
+
+class VxlanC(ctypes.Structure):
+    _fields_ = [("flags", ctypes.c_uint16), ("group_policy_id", ctypes.c_uint16),
+                ("raw_network_identifier", ctypes.c_uint32), ("network_identifier", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("payload_offset", _u64), ("payload_length", _u64)]
+
+
 assert ctypes.sizeof(GlobalHeaderC) == 24 and ctypes.sizeof(RecordC) == 24 and ctypes.sizeof(ShardC) == 48
+assert (ctypes.sizeof(VlanTagC), ctypes.sizeof(EthernetC), ctypes.sizeof(IPv4C), ctypes.sizeof(IPv6C),
+        ctypes.sizeof(ArpC), ctypes.sizeof(TcpC), ctypes.sizeof(UdpC), ctypes.sizeof(VxlanC)) == \
+    (8, 40, 72, 56, 22, 64, 24, 32)
 
 # Every symbol include/npr.h declares (checked by tests/test_abi.py).
 EXPORTED = [
@@ -117,6 +175,8 @@ EXPORTED = [
     "npr_dev_convert_records", "npr_dev_vxlan_flows", "npr_vxlan_flows", "npr_dev_flow_aggregate",
     "npr_flow_details", "npr_dev_flow_details", "npr_dev_parse_extract_batch", "npr_shm_all_gather",
     "npr_stream_release", "npr_ctx_forget_density",
+    "npr_ethernet_parse", "npr_ipv4_parse", "npr_ipv6_parse", "npr_arp_parse", "npr_tcp_parse", "npr_udp_parse",
+    "npr_vxlan_parse",
 ]
 
 _c_size_p = ctypes.POINTER(ctypes.c_size_t)
@@ -179,6 +239,13 @@ _SIGNATURES = {
     "npr_dev_parse_extract_batch": (ctypes.c_int, [_vp, _vp, ctypes.c_uint32, _vp]),
     "npr_stream_release": (ctypes.c_int, [_vp, _vp]),
     "npr_ctx_forget_density": (ctypes.c_int, [_vp, _vp]),
+    "npr_ethernet_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.POINTER(EthernetC), _vp, ctypes.c_size_t,
+                                          _c_size_p, ctypes.POINTER(ctypes.c_uint64)]),
+    **{f"npr_{k}_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.POINTER(c), _c_size_p,
+                                         ctypes.POINTER(ctypes.c_uint64)])
+       for k, c in (("ipv4", IPv4C), ("ipv6", IPv6C), ("arp", ArpC), ("tcp", TcpC), ("udp", UdpC))},
+    "npr_vxlan_parse": (ctypes.c_int, [_u8p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(VxlanC), _c_size_p,
+                                       ctypes.POINTER(ctypes.c_uint64)]),
     "npr_shm_all_gather": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                           ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
 }

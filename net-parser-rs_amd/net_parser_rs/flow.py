@@ -180,15 +180,21 @@ class Vxlan:
 
     @staticmethod
     def parse(data, endianness):
-        """Vxlan::parse (:31-48): (remainder, Vxlan); fewer than 8 bytes raise
-        net_parser_rs.Incomplete, like nom's u16!/u32! (the remainder is always empty: rest)."""
-        from . import Endianness, Incomplete
-        data = bytes(data)
-        if len(data) < 8:
-            raise Incomplete()
-        e = ">" if endianness == Endianness.Big else "<"
-        flags, gpid, raw = struct.unpack(e + "HHI", data[:8])
-        return b"", Vxlan(flags, gpid, raw, data[8:])
+        """Vxlan::parse (:31-48) by npr_vxlan_parse: (remainder, Vxlan); a short header raises
+        net_parser_rs.Incomplete with nom's Needed::Size (u16!: 2, u32!: 4); the remainder is always
+        empty (rest)."""
+        from . import Incomplete, DeviceError
+        buf = bytes(data)
+        arr = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+        o, used, det = _abi.VxlanC(), ctypes.c_size_t(0), ctypes.c_uint64(0)
+        st = _abi.load_library().npr_vxlan_parse(ctypes.addressof(arr), len(buf), int(endianness), ctypes.byref(o),
+                                                 ctypes.byref(used), ctypes.byref(det))
+        if st == _abi.INCOMPLETE:
+            raise Incomplete(det.value)
+        if st != _abi.OK:
+            raise DeviceError(f"npr_vxlan_parse status {st}")
+        return buf[used.value:], Vxlan(o.flags, o.group_policy_id, o.raw_network_identifier,
+                                       buf[o.payload_offset:o.payload_offset + o.payload_length])
 
     def as_bytes(self):
         """Vxlan::as_bytes (:18-29): big-endian header + payload."""

@@ -1,58 +1,62 @@
-"""net_parser_rs.layers — host mirror of the reference's per-layer header objects and their
-`as_bytes` serializers: Ethernet (src/layer2/ethernet.rs), IPv4
-(src/layer3/ipv4.rs), Tcp / Udp (src/layer4/{tcp,udp}.rs) and the Layer4 dispatch
-(src/layer4/mod.rs:14-27).
+"""net_parser_rs.layers — the reference's per-layer header objects:
+Ethernet (src/layer2/ethernet.rs), IPv4 / IPv6 / Arp (src/layer3/{ipv4,ipv6,arp}.rs), Tcp / Udp
+(src/layer4/{tcp,udp}.rs) and the Layer4 dispatch (src/layer4/mod.rs:14-27), with their `as_bytes`
+serializers where the reference has them.
 
-These parse ONE header object from a byte string, like GlobalHeader::parse: an object API for
-callers that inspect or rebuild frames.  The flows of whole captures never come from here; they come
-from the device (extract_flow / convert_records over libnpr.so).  Each step follows the reference's
-nom 4 chain in order, with its quirks (release-build wrapping arithmetic):
+Each `parse` reads ONE header object through libnpr's host-side layer parsers (npr_ethernet_parse,
+npr_ipv4_parse, ... in csrc/npr_layers.hip; no device work): an object API for callers that inspect
+or rebuild frames.  The flows of whole captures never come from here; they come from the device
+(extract_flow / convert_records).  The parsers follow the reference's nom 4 chains in order, with
+its quirks (release-build wrapping arithmetic):
 - Ethernet: a VLAN tag's prio / dei are `(total & 0x7000) as u8` / `(total & 0x8000) as u8`, i.e. 0;
 - IPv4: the payload is `total_length - header_length` (u16, wrapping) bytes taken right after the
   20-byte header, THEN the options, then trailing padding; as_bytes writes them in that order;
+- IPv6: one next-header byte per "extension" header (quirk Q11);
 - Udp: the payload is `length - 8` bytes (usize, wrapping: a length below 8 asks for ~2^64 bytes).
 Errors are the reference's (src/errors.rs:3-55): Incomplete(size) for nom's Needed::Size, Failure
-for a nom Error (an unknown EtherType / IP protocol, a TCP header length outside 20..60), Custom for
-IPv4's version check.
+"Error: Code(<input>, MapOpt|MapRes)" for a map_opt! / map_res! (an unknown EtherType / IP protocol,
+a TCP header length outside 20..60), Custom for the IP version checks.
 """
 import ipaddress
 import struct
 
-from . import Custom, Failure, Incomplete
+import ctypes
+
+from . import Custom, DeviceError, Failure, Incomplete, _abi
 from .flow import MacAddress, Vxlan
 
-__all__ = ["EthernetTypeId", "VlanTag", "Ethernet", "InternetProtocolId", "IPv4", "Tcp", "Udp", "Layer4"]
+__all__ = ["EthernetTypeId", "VlanTag", "Ethernet", "InternetProtocolId", "IPv4", "IPv6", "Arp", "Tcp", "Udp",
+           "Layer4"]
 
 _U64 = (1 << 64) - 1
 
 
-class _Reader:
-    """nom 4's big-endian number parsers and take! over a byte string (Needed::Size on short input)."""
-    __slots__ = ("b", "i")
+def _call(name, data, out, *mid):
+    """libnpr's host parser `name` over `data`: (the input bytes, *consumed) or the reference's error.
+    `mid` are the arguments between the output struct and (consumed, detail)."""
+    buf = bytes(data)
+    arr = (ctypes.c_uint8 * max(len(buf), 1)).from_buffer_copy(buf or b"\0")
+    used, det = ctypes.c_size_t(0), ctypes.c_uint64(0)
+    st = getattr(_abi.load_library(), name)(ctypes.addressof(arr), len(buf), ctypes.byref(out), *mid,
+                                           ctypes.byref(used), ctypes.byref(det))
+    return buf, used.value, st, det.value
 
-    def __init__(self, data):
-        self.b, self.i = bytes(data), 0
 
-    def take(self, n):
-        if len(self.b) - self.i < n:
-            raise Incomplete(n)
-        out = self.b[self.i:self.i + n]
-        self.i += n
-        return out
+def _check(st, det, buf, kind, custom):
+    if st == _abi.OK or st == -3:  # NPR_ERR_CAPACITY: the caller asks again with room
+        return
+    if st == _abi.INCOMPLETE:
+        raise Incomplete(det)
+    if st == _abi.FAILURE:  # nom's Context::Code(<the failing primitive's input>, kind)
+        a, b = det & 0xFFFFFFFF, det >> 32
+        raise Failure(f"Error: Code({list(buf[a:b])}, {kind})")
+    if st == _abi.CUSTOM:
+        raise Custom(custom.format(det))
+    raise DeviceError(f"{_abi.load_library()} layer parser status {st}")
 
-    def u8(self):
-        return self.take(1)[0]
 
-    def u16(self):
-        return struct.unpack(">H", self.take(2))[0]
-
-    def u32(self):
-        return struct.unpack(">I", self.take(4))[0]
-
-    def rest(self):
-        out = self.b[self.i:]
-        self.i = len(self.b)
-        return out
+def _slice(buf, off, n):
+    return buf[off:off + n]
 
 
 # ---- layer 2 ------------------------------------------------------------------------------------
@@ -109,18 +113,20 @@ class Ethernet:
 
     @staticmethod
     def parse(data):
-        """Ethernet::parse (:206-216): two MACs, then EtherType / VLAN tags until a non-VLAN type,
-        then the rest as payload.  -> (remainder, Ethernet); the remainder is always empty."""
-        r = _Reader(data)
-        dst, src = r.take(6), r.take(6)
-        vlans = []
-        while True:  # parse_vlan_tag (:163-204)
-            t = EthernetTypeId.new(r.u16())
-            if t is None:
-                raise Failure("Error: MapOpt")
-            if t.kind != "Vlan":
-                return b"", Ethernet(dst, src, t, vlans, r.rest())  # parse_not_vlan_tag (:140-161)
-            vlans.append(VlanTag(t, r.u16()))
+        """Ethernet::parse (:204-216) by npr_ethernet_parse: two MACs, then EtherType / VLAN tags until
+        a non-VLAN type, then the rest as payload.  -> (remainder, Ethernet); the remainder is always
+        empty."""
+        cap = 8
+        while True:
+            out, tags = _abi.EthernetC(), (_abi.VlanTagC * cap)()
+            buf, used, st, det = _call("npr_ethernet_parse", data, out, ctypes.addressof(tags), cap)
+            _check(st, det, buf, "MapOpt", "")
+            if out.n_vlans <= cap:
+                break
+            cap = out.n_vlans
+        vlans = [VlanTag(EthernetTypeId.new(t.vlan_type), t.vlan_value) for t in tags[:out.n_vlans]]
+        return buf[used:], Ethernet(bytes(out.dst_mac), bytes(out.src_mac), EthernetTypeId.new(out.ether_type), vlans,
+                                    _slice(buf, out.payload_offset, out.payload_length))
 
     def as_bytes(self):
         """Ethernet::as_bytes (:116-132)."""
@@ -172,32 +178,17 @@ class IPv4:
 
     @staticmethod
     def parse(data):
-        """IPv4::parse (:148-160) + parse_ipv4 (:76-146).  -> (remainder, IPv4)."""
-        data = bytes(data)
-        input_len = len(data)
-        r = _Reader(data)
-        vl = r.u8()
-        if vl >> 4 != 4:
-            raise Custom(f"Expected version 4, was {vl >> 4}")
-        words = vl & 0x0F
-        header_length = words * 4
-        additional = (words - 5) * 4 if words > 5 else 0
-        tos = r.u8()
-        raw_length = r.u16()
-        length = (raw_length - header_length) & 0xFFFF  # u16 subtraction, wrapping (:97-101)
-        expected = header_length + additional + length
-        ident, flags, ttl = r.u16(), r.u16(), r.u8()
-        protocol = InternetProtocolId.new(r.u8())
-        if protocol is None:
-            raise Failure("Error: MapOpt")
-        checksum = r.u16()
-        src, dst = ipaddress.IPv4Address(r.take(4)), ipaddress.IPv4Address(r.take(4))
-        payload = r.take(length)
-        options = r.take(additional) if additional > 0 else None
-        padding = r.take(input_len - expected) if input_len > expected else None
-        return r.rest(), IPv4(version_and_length=vl, tos=tos, raw_length=raw_length, id=ident, flags=flags, ttl=ttl,
-                              protocol=protocol, checksum=checksum, src_ip=src, dst_ip=dst, payload=payload,
-                              options=options, padding=padding)
+        """IPv4::parse (:148-160) + parse_ipv4 (:76-146) by npr_ipv4_parse.  -> (remainder, IPv4)."""
+        o = _abi.IPv4C()
+        buf, used, st, det = _call("npr_ipv4_parse", data, o)
+        _check(st, det, buf, "MapOpt", "Expected version 4, was {}")
+        return buf[used:], IPv4(version_and_length=o.version_and_length, tos=o.tos, raw_length=o.raw_length, id=o.id,
+                                flags=o.flags, ttl=o.ttl, protocol=InternetProtocolId(o.protocol), checksum=o.checksum,
+                                src_ip=ipaddress.IPv4Address(bytes(o.src_ip)),
+                                dst_ip=ipaddress.IPv4Address(bytes(o.dst_ip)),
+                                payload=_slice(buf, o.payload_offset, o.payload_length),
+                                options=_slice(buf, o.options_offset, o.options_length) if o.options_length else None,
+                                padding=_slice(buf, o.padding_offset, o.padding_length) if o.padding_length else None)
 
     def as_bytes(self):
         """IPv4::as_bytes (:42-74): header fields, addresses, payload, options, padding."""
@@ -205,6 +196,42 @@ class IPv4:
                           self.ttl, self.protocol.value(), self.checksum)
         out += self.src_ip.packed + self.dst_ip.packed + self.payload
         return out + (self.options or b"") + (self.padding or b"")
+
+
+class IPv6:
+    """IPv6 (src/layer3/ipv6.rs:10-16).  The reference has no serializer for it."""
+    __slots__ = ("dst_ip", "src_ip", "protocol", "payload")
+
+    def __init__(self, dst_ip, src_ip, protocol, payload):
+        self.dst_ip, self.src_ip, self.protocol, self.payload = dst_ip, src_ip, protocol, payload
+
+    @staticmethod
+    def parse(data):
+        """IPv6::parse (:87-99) by npr_ipv6_parse: version 6, flow label, payload length, the next
+        header (one byte per "extension" header), hop limit, the addresses, take!(payload length)."""
+        o = _abi.IPv6C()
+        buf, used, st, det = _call("npr_ipv6_parse", data, o)
+        _check(st, det, buf, "MapOpt", "Expected version 6, version was {}")
+        return buf[used:], IPv6(ipaddress.IPv6Address(bytes(o.dst_ip)), ipaddress.IPv6Address(bytes(o.src_ip)),
+                                InternetProtocolId(o.protocol), _slice(buf, o.payload_offset, o.payload_length))
+
+
+class Arp:
+    """Arp (src/layer3/arp.rs:7-14).  The reference has no serializer for it."""
+    __slots__ = ("sender_ip", "sender_mac", "target_ip", "target_mac", "operation")
+
+    def __init__(self, sender_ip, sender_mac, target_ip, target_mac, operation):
+        self.sender_ip, self.sender_mac, self.target_ip = sender_ip, MacAddress(sender_mac), target_ip
+        self.target_mac, self.operation = MacAddress(target_mac), operation
+
+    @staticmethod
+    def parse(data):
+        """Arp::parse (:54-76) by npr_arp_parse."""
+        o = _abi.ArpC()
+        buf, used, st, det = _call("npr_arp_parse", data, o)
+        _check(st, det, buf, "MapOpt", "")
+        return buf[used:], Arp(ipaddress.IPv4Address(bytes(o.sender_ip)), bytes(o.sender_mac),
+                               ipaddress.IPv4Address(bytes(o.target_ip)), bytes(o.target_mac), o.operation)
 
 
 # ---- layer 4 ------------------------------------------------------------------------------------
@@ -223,18 +250,17 @@ class Tcp:
 
     @staticmethod
     def parse(data):
-        """Tcp::parse (:54-101): a header length outside 20..60 is a nom Error; payload = rest."""
-        r = _Reader(data)
-        src, dst, seq, ack = r.u16(), r.u16(), r.u32(), r.u32()
-        v = r.u16()
-        hl = Tcp.extract_length(v)
-        if not 20 <= hl <= 60:
-            raise Failure("Error: MapRes")
-        window, check, urgent = r.u16(), r.u16(), r.u16()
-        options = r.take(hl - 20)
-        return b"", Tcp(src_port=src, dst_port=dst, sequence_number=seq, acknowledgement_number=ack,
-                        header_length_and_flags=v, header_length=hl, flags=v & 0x01FF, window=window, check=check,
-                        urgent=urgent, options=options, payload=r.rest())
+        """Tcp::parse (:54-101) by npr_tcp_parse: a header length outside 20..60 is a map_res!
+        Failure; payload = rest.  -> (remainder, Tcp)."""
+        o = _abi.TcpC()
+        buf, used, st, det = _call("npr_tcp_parse", data, o)
+        _check(st, det, buf, "MapRes", "")
+        return buf[used:], Tcp(src_port=o.src_port, dst_port=o.dst_port, sequence_number=o.sequence_number,
+                               acknowledgement_number=o.acknowledgement_number,
+                               header_length_and_flags=o.header_length_and_flags, header_length=o.header_length,
+                               flags=o.flags, window=o.window, check=o.check, urgent=o.urgent,
+                               options=_slice(buf, o.options_offset, o.options_length),
+                               payload=_slice(buf, o.payload_offset, o.payload_length))
 
     def as_bytes(self):
         """Tcp::as_bytes (:33-51)."""
@@ -252,13 +278,12 @@ class Udp:
 
     @staticmethod
     def parse(data):
-        """Udp::parse (:33-50): payload = take!(length - 8), usize wrapping.  -> (remainder, Udp)."""
-        r = _Reader(data)
-        src, dst = r.u16(), r.u16()
-        length = (r.u16() - 8) & _U64
-        checksum = r.u16()
-        payload = r.take(length)
-        return r.rest(), Udp(src, dst, checksum, payload)
+        """Udp::parse (:33-50) by npr_udp_parse: payload = take!(length - 8), usize wrapping.
+        -> (remainder, Udp)."""
+        o = _abi.UdpC()
+        buf, used, st, det = _call("npr_udp_parse", data, o)
+        _check(st, det, buf, "MapOpt", "")
+        return buf[used:], Udp(o.src_port, o.dst_port, o.checksum, _slice(buf, o.payload_offset, o.payload_length))
 
     def as_bytes(self):
         """Udp::as_bytes (:19-31): the length field is len(payload) + 8 (as u16)."""

@@ -1,4 +1,4 @@
-//! `extern "C"` view of include/npr.h (ABI 4): the entry points this crate binds, with the
+//! `extern "C"` view of include/npr.h (ABI 5): the entry points this crate binds, with the
 //! reference functions they replace.
 #![allow(non_camel_case_types)]
 
@@ -12,7 +12,7 @@ pub const NPR_CUSTOM: npr_status = 3; // Error::Custom (src/errors.rs:9)
 pub const NPR_ERR_CAPACITY: npr_status = -3;
 pub const NPR_LITTLE: c_int = 0;
 pub const NPR_BIG: c_int = 1;
-pub const NPR_ABI_VERSION: c_int = 4;
+pub const NPR_ABI_VERSION: c_int = 5;
 pub const NPR_FLOW_KIND_IPV6: u8 = 0x1;
 pub const NPR_FLOW_KIND_UDP: u8 = 0x2;
 
@@ -73,7 +73,155 @@ pub struct npr_flow_v6 {
     pub dst_ip: [u8; 16],
 }
 
+// ---- host-side per-layer header objects (include/npr.h): byte ranges are {offset, length} ----------
+/// VlanTag (src/layer2/ethernet.rs:85-98)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_vlan_tag {
+    pub vlan_type: u16,
+    pub vlan_value: u16,
+    pub prio: u8,
+    pub dei: u8,
+    pub id: u16,
+}
+
+/// Ethernet (src/layer2/ethernet.rs:100-107); the first min(n_vlans, cap) tags go to the tag array
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_ethernet {
+    pub dst_mac: [u8; 6],
+    pub src_mac: [u8; 6],
+    pub ether_type: u16,
+    pub reserved: u16,
+    pub n_vlans: u32,
+    pub payload_offset: u64,
+    pub payload_length: u64,
+}
+
+/// IPv4 (src/layer3/ipv4.rs:14-29); options / padding length 0 = None
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_ipv4 {
+    pub version_and_length: u8,
+    pub tos: u8,
+    pub raw_length: u16,
+    pub id: u16,
+    pub flags: u16,
+    pub ttl: u8,
+    pub protocol: u8,
+    pub checksum: u16,
+    pub src_ip: [u8; 4],
+    pub dst_ip: [u8; 4],
+    pub payload_offset: u64,
+    pub payload_length: u64,
+    pub options_offset: u64,
+    pub options_length: u64,
+    pub padding_offset: u64,
+    pub padding_length: u64,
+}
+
+/// IPv6 (src/layer3/ipv6.rs:10-16)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_ipv6 {
+    pub dst_ip: [u8; 16],
+    pub src_ip: [u8; 16],
+    pub protocol: u8,
+    pub reserved: [u8; 7],
+    pub payload_offset: u64,
+    pub payload_length: u64,
+}
+
+/// Arp (src/layer3/arp.rs:7-14)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_arp {
+    pub sender_ip: [u8; 4],
+    pub sender_mac: [u8; 6],
+    pub target_ip: [u8; 4],
+    pub target_mac: [u8; 6],
+    pub operation: u16,
+}
+
+/// Tcp (src/layer4/tcp.rs:11-30) with its HeaderLengthAndFlags
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_tcp {
+    pub src_port: u16,
+    pub dst_port: u16,
+    pub sequence_number: u32,
+    pub acknowledgement_number: u32,
+    pub header_length_and_flags: u16,
+    pub flags: u16,
+    pub header_length: u32,
+    pub window: u16,
+    pub check: u16,
+    pub urgent: u16,
+    pub reserved: u16,
+    pub options_offset: u64,
+    pub options_length: u64,
+    pub payload_offset: u64,
+    pub payload_length: u64,
+}
+
+/// Udp (src/layer4/udp.rs:10-16)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_udp {
+    pub src_port: u16,
+    pub dst_port: u16,
+    pub checksum: u16,
+    pub reserved: u16,
+    pub payload_offset: u64,
+    pub payload_length: u64,
+}
+
+/// Vxlan (src/layer4/vxlan.rs:7-14)
+#[repr(C)]
+#[derive(Clone, Copy, Default, Debug)]
+pub struct npr_vxlan {
+    pub flags: u16,
+    pub group_policy_id: u16,
+    pub raw_network_identifier: u32,
+    pub network_identifier: u32,
+    pub reserved: u32,
+    pub payload_offset: u64,
+    pub payload_length: u64,
+}
+
 extern "C" {
+    /// Ethernet::parse (src/layer2/ethernet.rs:204-216), host side.  Incomplete: *detail = nom's
+    /// Needed::Size; Failure: *detail = start | end << 32 of the map_opt! input; more tags than
+    /// vlan_cap: NPR_ERR_CAPACITY with the exact n_vlans
+    pub fn npr_ethernet_parse(
+        input: *const u8,
+        len: usize,
+        out: *mut npr_ethernet,
+        vlans: *mut npr_vlan_tag,
+        vlan_cap: usize,
+        consumed: *mut usize,
+        detail: *mut u64,
+    ) -> npr_status;
+    /// IPv4::parse (src/layer3/ipv4.rs:148-160); Custom: *detail = the version nibble
+    pub fn npr_ipv4_parse(input: *const u8, len: usize, out: *mut npr_ipv4, consumed: *mut usize, detail: *mut u64) -> npr_status;
+    /// IPv6::parse (src/layer3/ipv6.rs:87-99); Custom: *detail = the version nibble
+    pub fn npr_ipv6_parse(input: *const u8, len: usize, out: *mut npr_ipv6, consumed: *mut usize, detail: *mut u64) -> npr_status;
+    /// Arp::parse (src/layer3/arp.rs:54-76)
+    pub fn npr_arp_parse(input: *const u8, len: usize, out: *mut npr_arp, consumed: *mut usize, detail: *mut u64) -> npr_status;
+    /// Tcp::parse (src/layer4/tcp.rs:59-101); Failure = the map_res! on the header length
+    pub fn npr_tcp_parse(input: *const u8, len: usize, out: *mut npr_tcp, consumed: *mut usize, detail: *mut u64) -> npr_status;
+    /// Udp::parse (src/layer4/udp.rs:33-50)
+    pub fn npr_udp_parse(input: *const u8, len: usize, out: *mut npr_udp, consumed: *mut usize, detail: *mut u64) -> npr_status;
+    /// Vxlan::parse (src/layer4/vxlan.rs:31-48)
+    pub fn npr_vxlan_parse(
+        input: *const u8,
+        len: usize,
+        endianness: c_int,
+        out: *mut npr_vxlan,
+        consumed: *mut usize,
+        detail: *mut u64,
+    ) -> npr_status;
+
     /// GlobalHeader::parse (src/global_header.rs:40-70): 24 bytes, host side
     pub fn npr_global_header_parse(
         input: *const u8,

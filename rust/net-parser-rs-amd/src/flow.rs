@@ -387,7 +387,7 @@ fn flows_only(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<Vec<Option<Flo
 
 /// extract_flow over `payloads` (read from `input` when they lie inside it): one device call, plus
 /// one for the error payloads of the records that failed.
-fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<Vec<Result<Flow, Error>>, crate::Error> {
+pub(crate) fn extract_payloads(payloads: &[&[u8]], input: Option<&[u8]>) -> Result<Vec<Result<Flow, Error>>, crate::Error> {
     let n = payloads.len();
     if n == 0 {
         return Ok(Vec::new());

@@ -13,18 +13,17 @@
 //! every parse runs in libnpr.
 //!
 //! **Surface.**  This crate is a drop-in for the capture -> records -> flows path (the table below)
-//! and nothing else.  Code that uses only those items compiles unchanged.  NOT restated, because
-//! they are off that path ("out of scope"):
-//! - the per-layer parsers and their structs: `layer2::ethernet::Ethernet::parse`
-//!   (src/layer2/ethernet.rs:204), `layer3::{Arp, IPv4, IPv6}::parse` (src/layer3/arp.rs:54,
-//!   ipv4.rs:148, ipv6.rs:87), `layer4::{Tcp, Udp, Vxlan}::parse` (src/layer4/tcp.rs:59, udp.rs:33,
-//!   vxlan.rs:31).  Their error types and ids ARE here (a flow error names them);
-//! - `FlowExtraction` for those layer structs (src/flow/layer2/ethernet.rs:39 ... layer4/vxlan.rs:32):
-//!   it is implemented for [`PcapRecord`] (src/flow/mod.rs:44), the one the record path uses.  The
-//!   VXLAN inner-frame flow is [`flow::vxlan_flows`], batched.
-//!
-//! A crate that also calls the per-layer parsers keeps the reference for them, under a second
-//! dependency name (`net-parser-rs-ref = { package = "net-parser-rs", version = "0.3" }`).
+//! and the reference's per-layer header objects.  Code that uses those items compiles unchanged.
+//! - The per-layer parsers and their structs, under the reference's paths:
+//!   `layer2::ethernet::{Ethernet, VlanTag}` (src/layer2/ethernet.rs:84-217),
+//!   `layer3::{Arp, IPv4, IPv6, Layer3}` (src/layer3/{arp,ipv4,ipv6}.rs),
+//!   `layer4::{Tcp, Udp, Vxlan, Layer4}` (src/layer4/{tcp,udp,vxlan}.rs), with their `as_bytes`:
+//!   each `parse` runs libnpr's host-side layer parser (npr_ethernet_parse ... npr_vxlan_parse).
+//! - `flow::layer2::FlowExtraction` for `Ethernet` (src/flow/layer2/ethernet.rs:39): the frame's flow
+//!   from the device decoder.  NOT restated: the layer-3 / layer-4 `FlowExtraction` traits
+//!   (src/flow/layer3/mod.rs:9, src/flow/layer4/mod.rs:10), which build a flow from outer-layer
+//!   info structs; [`flow::FlowExtraction`] on [`PcapRecord`] and [`flow::vxlan_flows`] cover the
+//!   record path and the VXLAN inner flow.
 //!
 //! | reference (src file:line)                          | here                                            |
 //! |----------------------------------------------------|-------------------------------------------------|
@@ -52,6 +51,7 @@
 
 pub mod ffi;
 pub mod flow;
+mod layers;
 mod types;
 
 pub use types::{common, errors, layer2, layer3, layer4};

@@ -8,8 +8,9 @@
 //! | `common`                     | src/common.rs:3-26                                              |
 //! | `errors`                     | src/errors.rs:3-55                                              |
 //! | `global_header`              | src/global_header.rs:4-37 (parse: crate root, over the C-ABI)   |
-//! | `layer2::ethernet`           | src/layer2/ethernet.rs:16-98 (the EtherType ids)                |
-//! | `layer3`                     | src/layer3/mod.rs:25-84 (InternetProtocolId)                    |
+//! | `layer2::ethernet`           | src/layer2/ethernet.rs:16-98 (the EtherType ids; the structs: layers.rs) |
+//! | `layer3`                     | src/layer3/mod.rs:25-84 (InternetProtocolId; the structs: layers.rs) |
+//! | `layer4`                     | src/layer4 (the structs: layers.rs)                             |
 //! | `flow_types::{device, info}` | src/flow/device.rs:7-27, src/flow/info.rs:1-95                  |
 //! | `flow_types::errors` + tree  | src/flow/errors.rs:5-19 and the per-layer `errors` modules      |
 
@@ -175,8 +176,23 @@ pub mod layer2 {
                     _ => return None,
                 })
             }
+
+            /// EthernetTypeId::value (src/layer2/ethernet.rs:75-81)
+            pub(crate) fn value(&self) -> u16 {
+                match self {
+                    EthernetTypeId::PayloadLength(v) => *v,
+                    EthernetTypeId::Vlan(v) => v.value(),
+                    EthernetTypeId::L3(v) => v.value(),
+                }
+            }
         }
+
+        /// src/layer2/ethernet.rs:84-217 (parse over npr_ethernet_parse: crate::layers)
+        pub use crate::layers::{Ethernet, VlanTag};
     }
+
+    pub use crate::layers::Layer2;
+    pub use ethernet::Ethernet;
 }
 
 /// src/layer3/mod.rs: IP protocol numbers
@@ -231,11 +247,33 @@ pub mod layer3 {
             )
         }
     }
+
+    /// src/layer3/{arp,ipv4,ipv6}.rs (parse over npr_arp_parse / npr_ipv4_parse / npr_ipv6_parse)
+    pub mod arp {
+        pub use crate::layers::Arp;
+    }
+    pub mod ipv4 {
+        pub use crate::layers::IPv4;
+    }
+    pub mod ipv6 {
+        pub use crate::layers::IPv6;
+    }
+    pub use crate::layers::{Arp, IPv4, IPv6, Layer3};
 }
 
-/// src/layer4: the reference's TCP / UDP / VXLAN header parsers are not part of this drop-in (the
-/// flow path decodes them on the device); the module is kept so paths under it still resolve.
-pub mod layer4 {}
+/// src/layer4/{tcp,udp,vxlan}.rs (parse over npr_tcp_parse / npr_udp_parse / npr_vxlan_parse)
+pub mod layer4 {
+    pub mod tcp {
+        pub use crate::layers::{HeaderLengthAndFlags, Tcp};
+    }
+    pub mod udp {
+        pub use crate::layers::Udp;
+    }
+    pub mod vxlan {
+        pub use crate::layers::Vxlan;
+    }
+    pub use crate::layers::{Layer4, Tcp, Udp, Vxlan};
+}
 
 /// src/flow/{device,info,errors}.rs and the per-layer `errors` modules of src/flow/layer{2,3,4}
 pub mod flow_types {
@@ -440,6 +478,11 @@ pub mod flow_types {
 
     /// src/flow/layer2/{mod,ethernet}.rs
     pub mod layer2 {
+        /// src/flow/layer2/mod.rs:6-8 (implemented for layer2::Ethernet in crate::layers)
+        pub trait FlowExtraction {
+            fn extract_flow(&self) -> Result<crate::flow::Flow, crate::flow::errors::Error>;
+        }
+
         pub mod errors {
             wrap!(Error { Ethernet(super::ethernet::errors::Error) => "Ethernet Error" });
         }

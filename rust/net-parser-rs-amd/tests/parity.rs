@@ -244,3 +244,65 @@ fn vxlan_inner_flows_match_reference() {
         }
     }
 }
+
+#[test]
+fn layer_objects_match_reference() {
+    // Ethernet / IPv4 / IPv6 / Arp / Tcp / Udp / Vxlan ::parse over every frame of the capture and
+    // over every prefix of a few: the same objects (Debug), the same errors, the same as_bytes
+    let data = capture();
+    let (_, fa) = net_parser_rs::CaptureFile::parse(&data).unwrap();
+    let recs = fa.records.into_inner();
+    let mut frames: Vec<&[u8]> = recs.iter().map(|r| r.payload).collect();
+    for f in recs.iter().take(40).map(|r| r.payload) {
+        for k in 0..f.len() {
+            frames.push(&f[..k]);
+        }
+    }
+    for (i, f) in frames.iter().enumerate() {
+        let a = amd::layer2::ethernet::Ethernet::parse(f);
+        let r = net_parser_rs::layer2::ethernet::Ethernet::parse(f);
+        assert_eq!(format!("{:?}", a), format!("{:?}", r), "ethernet {}", i);
+        let (pa, pr) = match (a, r) {
+            (Ok((_, a)), Ok((_, r))) => {
+                assert_eq!(a.as_bytes(), r.as_bytes(), "ethernet as_bytes {}", i);
+                (a.payload, r.payload)
+            }
+            _ => continue,
+        };
+        let a4 = amd::layer3::ipv4::IPv4::parse(pa);
+        let r4 = net_parser_rs::layer3::ipv4::IPv4::parse(pr);
+        assert_eq!(format!("{:?}", a4), format!("{:?}", r4), "ipv4 {}", i);
+        assert_eq!(format!("{:?}", amd::layer3::ipv6::IPv6::parse(pa)), format!("{:?}", net_parser_rs::layer3::ipv6::IPv6::parse(pr)), "ipv6 {}", i);
+        assert_eq!(format!("{:?}", amd::layer3::arp::Arp::parse(pa)), format!("{:?}", net_parser_rs::layer3::arp::Arp::parse(pr)), "arp {}", i);
+        if let (Ok((_, a4)), Ok((_, r4))) = (a4, r4) {
+            assert_eq!(a4.as_bytes(), r4.as_bytes(), "ipv4 as_bytes {}", i);
+            let (at, rt) = (amd::layer4::tcp::Tcp::parse(a4.payload), net_parser_rs::layer4::tcp::Tcp::parse(r4.payload));
+            assert_eq!(format!("{:?}", at), format!("{:?}", rt), "tcp {}", i);
+            let (au, ru) = (amd::layer4::udp::Udp::parse(a4.payload), net_parser_rs::layer4::udp::Udp::parse(r4.payload));
+            assert_eq!(format!("{:?}", au), format!("{:?}", ru), "udp {}", i);
+            for e in [nom::Endianness::Big, nom::Endianness::Little].iter() {
+                assert_eq!(
+                    format!("{:?}", amd::layer4::vxlan::Vxlan::parse(a4.payload, *e)),
+                    format!("{:?}", net_parser_rs::layer4::vxlan::Vxlan::parse(r4.payload, *e)),
+                    "vxlan {}",
+                    i
+                );
+            }
+        }
+    }
+}
+
+#[test]
+fn ethernet_flow_extraction_matches_reference() {
+    use amd::flow::layer2::FlowExtraction as _;
+    let data = capture();
+    let (_, fa) = net_parser_rs::CaptureFile::parse(&data).unwrap();
+    for r in fa.records.into_inner().iter().take(500) {
+        if let (Ok((_, a)), Ok((_, b))) =
+            (amd::layer2::ethernet::Ethernet::parse(r.payload), net_parser_rs::layer2::ethernet::Ethernet::parse(r.payload))
+        {
+            use net_parser_rs::flow::layer2::FlowExtraction as RefL2;
+            assert_eq!(format!("{:?}", a.extract_flow()), format!("{:?}", RefL2::extract_flow(&b)));
+        }
+    }
+}

@@ -45,6 +45,51 @@ static int same_flows(const npr_flow *a, const npr_flow_v6 *a6, const npr_flow *
   return 1;
 }
 
+/* The flow of one frame composed from the per-layer host parsers, as the src/flow/layer2..4 modules
+ * compose Ethernet -> IPv4 | IPv6 -> TCP | UDP (remainder checks included): 1 = a flow, 0 = an error. */
+static int layers_flow(const uint8_t *fr, size_t n, npr_flow *f, npr_flow_v6 *f6) {
+  npr_ethernet e;
+  npr_vlan_tag tag[8];
+  size_t used;
+  uint64_t det;
+  memset(f, 0, sizeof *f), memset(f6, 0, sizeof *f6);
+  const npr_status se = npr_ethernet_parse(fr, n, &e, tag, 8, &used, &det);
+  if (se != NPR_OK && se != NPR_ERR_CAPACITY) return 0;
+  const uint8_t *p = fr + e.payload_offset;
+  const uint64_t pn = e.payload_length;
+  uint64_t l4off, l4len;
+  int proto;
+  if (e.ether_type == 0x0800) {
+    npr_ipv4 v;
+    if (npr_ipv4_parse(p, pn, &v, &used, &det) != NPR_OK || used != pn) return 0;
+    memcpy(f->src_ip, v.src_ip, 4), memcpy(f->dst_ip, v.dst_ip, 4);
+    l4off = v.payload_offset, l4len = v.payload_length, proto = v.protocol;
+  } else if (e.ether_type == 0x86DD) {
+    npr_ipv6 v;
+    if (npr_ipv6_parse(p, pn, &v, &used, &det) != NPR_OK || used != pn) return 0;
+    memcpy(f6->src_ip, v.src_ip, 16), memcpy(f6->dst_ip, v.dst_ip, 16);
+    f->kind |= NPR_FLOW_KIND_IPV6;
+    l4off = v.payload_offset, l4len = v.payload_length, proto = v.protocol;
+  } else {
+    return 0;  /* ARP never yields a flow; LLDP / 802.3 lengths are L2 errors */
+  }
+  if (proto == 6) {
+    npr_tcp t;
+    if (npr_tcp_parse(p + l4off, l4len, &t, &used, &det) != NPR_OK) return 0;
+    f->src_port = t.src_port, f->dst_port = t.dst_port;
+  } else if (proto == 17) {
+    npr_udp u;
+    if (npr_udp_parse(p + l4off, l4len, &u, &used, &det) != NPR_OK || used != l4len) return 0;
+    f->src_port = u.src_port, f->dst_port = u.dst_port;
+    f->kind |= NPR_FLOW_KIND_UDP;
+  } else {
+    return 0;
+  }
+  memcpy(f->src_mac, e.src_mac, 6), memcpy(f->dst_mac, e.dst_mac, 6);
+  f->vlan = e.n_vlans ? tag[0].id : 0;
+  return 1;
+}
+
 static void run(npr_ctx *ctx, const char *path) {
   size_t len = 0;
   uint8_t *in = slurp(path, &len);
@@ -61,6 +106,23 @@ static void run(npr_ctx *ctx, const char *path) {
   size_t on = 0, ocons = 0;
   const int orc = or_capture_file_parse(in, len, &oh, orec, cap, &on, &ocons);
   const size_t onf = orc == OR_OK ? or_convert_records(in, len, orec, on, ofl, ofl6, cap) : 0;
+
+  /* the per-layer host parsers, composed, agree with the oracle's extract_flow on every record */
+  if (orc == OR_OK) {
+    size_t agree = 0;
+    for (size_t i = 0; i < on; ++i) {
+      const uint8_t *fr = in + orec[i].offset + 16;
+      npr_flow lf, of;
+      npr_flow_v6 lf6, of6;
+      const int ok = layers_flow(fr, orec[i].actual_length, &lf, &lf6);
+      const int ost = or_extract_flow(fr, orec[i].actual_length, 0, &of, &of6);
+      memset(of.record_offset, 0, 5), memset(lf.record_offset, 0, 5);
+      const int same = ok == (ost == 0) && (!ok || (!memcmp(&lf, &of, sizeof lf) &&
+                                                    (!(of.kind & NPR_FLOW_KIND_IPV6) || !memcmp(&lf6, &of6, sizeof lf6))));
+      agree += same;
+    }
+    CHECK(agree == on, "%s: layer parsers agree with extract_flow on %zu of %zu records", path, agree, on);
+  }
 
   /* GlobalHeader::parse (src/global_header.rs:40-70) */
   npr_global_header h;
@@ -214,6 +276,23 @@ done:
 int main(int argc, char **argv) {
   CHECK(npr_abi_version() == NPR_ABI_VERSION, "ABI %d vs header %d", npr_abi_version(), NPR_ABI_VERSION);
   printf("%s\n", npr_version());
+  {
+    /* Arp::parse on the reference's own frame (src/layer3/arp.rs:96-122) */
+    static const uint8_t arp[] = {0x00, 0x01, 0x08, 0x00, 0x06, 0x04, 0x00, 0x01, 0x00, 0x0a, 0xdc, 0x64, 0x85, 0xc2,
+                                  0xc0, 0xa8, 0x59, 0x01, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0xc0, 0xa8, 0x59, 0x02};
+    npr_arp a;
+    size_t used = 0;
+    uint64_t det = 0;
+    CHECK(npr_arp_parse(arp, sizeof arp, &a, &used, &det) == NPR_OK && used == sizeof arp && a.operation == 1 &&
+              a.sender_ip[3] == 1 && a.target_ip[3] == 2 && a.sender_mac[5] == 0xc2,
+          "arp_parse on the reference's frame");
+    CHECK(npr_arp_parse(arp, 27, &a, &used, &det) == NPR_INCOMPLETE && det == 4, "arp_parse short: Needed 4");
+    static const uint8_t vx[] = {0x08, 0x00, 0x00, 0x00, 0x00, 0x00, 0x7b, 0x00, 'x'};
+    npr_vxlan v;
+    CHECK(npr_vxlan_parse(vx, sizeof vx, NPR_BIG, &v, &used, &det) == NPR_OK && v.network_identifier == 123 &&
+              v.payload_offset == 8 && v.payload_length == 1,
+          "vxlan_parse: VNI 123 (src/layer4/vxlan.rs:63-90)");
+  }
   npr_ctx *ctx = NULL, *bad = (npr_ctx *)&failures;
   /* a device that does not exist: an error and no context, never a context that answers "empty" */
   CHECK(npr_ctx_create(4096, &bad) == NPR_ERR_DEVICE && bad == NULL, "ctx_create(4096) must fail");

@@ -61,7 +61,7 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global
 
 def test_abi_version():
     lib = _abi.load_library()
-    assert lib.npr_abi_version() == 4
+    assert lib.npr_abi_version() == 5
     assert b"gfx950" in lib.npr_version()
 
 
