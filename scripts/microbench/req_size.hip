@@ -54,6 +54,14 @@ __global__ __launch_bounds__(256) void k_req(const uint8_t *buf, uint64_t nlines
       u32x4 v;
       asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(a) : "memory");
       acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    } else if (M == 'F' || M == 'G') {  // an 80-B (F) / 64-B (G) window at a random 16-B aligned position
+      const uint8_t *w = buf + ((h % (nlines * 8 - 8)) * 16);
+      const __attribute__((address_space(1))) u32x4 *q = (const __attribute__((address_space(1))) u32x4 *)(uintptr_t)w;
+#pragma unroll
+      for (int k = 0; k < (M == 'F' ? 5 : 4); ++k) {
+        const u32x4 v = q[k];
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+      }
     } else {
       acc += *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)a;
     }
@@ -92,6 +100,12 @@ int main(int argc, char **argv) {
            loads * 128 / us / 1e3);
   };
   show("D dwordx4", run<'D'>(buf, nlines, out, threads));
+  {  // windows: lines touched = 1 + P(the window crosses a line end)
+    const float f = run<'F'>(buf, nlines, out, threads), g = run<'G'>(buf, nlines, out, threads);
+    const double lf = loads * (1.0 + 79.0 / 128.0 * 0 + (8.0 - 3.0) / 8.0), lg = loads * (1.0 + (8.0 - 4.0) / 8.0);
+    printf("%-28s %8.1f us  %6.2f G windows/s %6.2f G lines/s\n", "F 80-B windows (5 x dwordx4)", f, loads / f / 1e3, lf / f / 1e3);
+    printf("%-28s %8.1f us  %6.2f G windows/s %6.2f G lines/s\n", "G 64-B windows (4 x dwordx4)", g, loads / g / 1e3, lg / g / 1e3);
+  }
   if (argc > 2) {  // sizes sweep: the default form only
     CK(hipFree(buf));
     CK(hipFree(out));
