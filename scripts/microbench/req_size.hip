@@ -34,7 +34,7 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
 template <char M>
 __global__ __launch_bounds__(256) void k_req(const uint8_t *buf, uint64_t nlines, uint32_t *out, uint32_t salt) {
   const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  uint32_t acc = 0;
+  uint32_t acc = 0, bad = 0;
 #pragma unroll
   for (int j = 0; j < kPer; ++j) {
     const uint64_t h = mix(t * kPer + j + ((uint64_t)salt << 40));
@@ -54,6 +54,18 @@ __global__ __launch_bounds__(256) void k_req(const uint8_t *buf, uint64_t nlines
       u32x4 v;
       asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(a) : "memory");
       acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+    } else if (M == 'H') {  // 64 B at a random BYTE position: four unaligned dwordx4 loads
+      const uint64_t pb = h % (nlines * 128 - 64);
+      const __attribute__((address_space(1))) u32x4 *q = (const __attribute__((address_space(1))) u32x4 *)(uintptr_t)(buf + pb);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32x4 v = q[k];
+        acc += v[0] ^ v[1] ^ v[2] ^ v[3];
+        if (k == 0) {  // the byte pattern buf[i] = i * 7 (mod 256): the first word must match it
+          const uint32_t b0 = (uint32_t)(pb * 7), want = (b0 & 255) | ((b0 + 7) & 255) << 8 | ((b0 + 14) & 255) << 16 | ((b0 + 21) & 255) << 24;
+          bad += v[0] != want;
+        }
+      }
     } else if (M == 'F' || M == 'G') {  // an 80-B (F) / 64-B (G) window at a random 16-B aligned position
       const uint8_t *w = buf + ((h % (nlines * 8 - 8)) * 16);
       const __attribute__((address_space(1))) u32x4 *q = (const __attribute__((address_space(1))) u32x4 *)(uintptr_t)w;
@@ -66,7 +78,11 @@ __global__ __launch_bounds__(256) void k_req(const uint8_t *buf, uint64_t nlines
       acc += *(const __attribute__((address_space(1))) uint32_t *)(uintptr_t)a;
     }
   }
-  out[t] = acc;
+  out[t] = M == 'H' ? (bad << 24) + (acc & 0xffffffu) : acc;
+}
+
+__global__ void k_fill(uint8_t *buf, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) buf[i] = (uint8_t)(i * 7);
 }
 
 template <char M>
@@ -93,7 +109,8 @@ int main(int argc, char **argv) {
   uint32_t *out;
   CK(hipMalloc(&buf, bytes));
   CK(hipMalloc(&out, threads * 4ull));
-  CK(hipMemset(buf, 1, bytes));
+  hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, buf, bytes);
+  CK(hipDeviceSynchronize());
   const double loads = (double)threads * kPer;
   auto show = [&](const char *name, float us) {
     printf("%-28s %8.1f us  %6.2f G loads/s  %7.1f GB/s of 128-B lines\n", name, us, loads / us / 1e3,
@@ -105,6 +122,14 @@ int main(int argc, char **argv) {
     const double lf = loads * (1.0 + 79.0 / 128.0 * 0 + (8.0 - 3.0) / 8.0), lg = loads * (1.0 + (8.0 - 4.0) / 8.0);
     printf("%-28s %8.1f us  %6.2f G windows/s %6.2f G lines/s\n", "F 80-B windows (5 x dwordx4)", f, loads / f / 1e3, lf / f / 1e3);
     printf("%-28s %8.1f us  %6.2f G windows/s %6.2f G lines/s\n", "G 64-B windows (4 x dwordx4)", g, loads / g / 1e3, lg / g / 1e3);
+    const float hh = run<'H'>(buf, nlines, out, threads);
+    uint32_t *ho = (uint32_t *)malloc(threads * 4ull);
+    CK(hipMemcpy(ho, out, threads * 4ull, hipMemcpyDeviceToHost));
+    uint64_t nbad = 0;
+    for (uint32_t i = 0; i < threads; ++i) nbad += ho[i] >> 24;
+    free(ho);
+    printf("%-28s %8.1f us  %6.2f G windows/s %6.2f G lines/s  (%llu wrong words)\n", "H 64 B unaligned (4 x dwordx4)", hh,
+           loads / hh / 1e3, loads * (1.0 + 63.0 / 128.0) / hh / 1e3, (unsigned long long)nbad);
   }
   if (argc > 2) {  // sizes sweep: the default form only
     CK(hipFree(buf));
