@@ -1696,12 +1696,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   if (lane == 0) sh.prog[wid] = ~0u;  // done: no longer the slowest
   if (DIAG) stamp_at(st, 2);
   const uint32_t ep = kp.epoch;
-  if (active && lane == 0) {  // A: in LDS for the workgroup fold, in HBM for the rare generic prefix
-    RangeSlot *rs = kp.rslots + v;
-    st_agent(&rs->a[0], gran(ep, pos == kNone ? 0ull : pos));
-    st_agent(&rs->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
-    st_agent(&rs->a[2], gran(ep, cnt));
-    st_agent(&rs->a[3], gran(ep, okc));
+  if (active && lane == 0) {  // A: in LDS for the workgroup fold (in HBM after the barrier, below)
     Seg A;
     A.entry = entry;
     A.exit = pos == kNone ? 0ull : pos;
@@ -1715,6 +1710,16 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
+  // A in HBM, for the rare generic prefix of another range (its readers wait for the epoch tags).
+  // Stored after the barrier: the barrier's release fence waits for every store issued before it,
+  // and write-through stores held the workgroup's fold back by their round trip.
+  if (active && lane == 0) {
+    RangeSlot *rs = kp.rslots + v;
+    st_agent(&rs->a[0], gran(ep, pos == kNone ? 0ull : pos));
+    st_agent(&rs->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
+    st_agent(&rs->a[2], gran(ep, cnt));
+    st_agent(&rs->a[3], gran(ep, okc));
+  }
   if (wid == 0) {
     // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
     // flows wait there, so the windows get the registers.
