@@ -23,7 +23,7 @@ NPR_HD uint32_t be16_of(uint32_t w) { return ((w & 0xffu) << 8) | ((w >> 8) & 0x
 // step decides between Incomplete / Failure / Custom.
 // ---------------------------------------------------------------------------------------------
 struct FlowWords {
-  uint32_t d[7];
+  uint32_t d[8];  // d[7] unused: keeps put_flow's 16-B row halves inside d (else the widened load spans into v6 and pins both in scratch)
   uint32_t v6[8];
   uint32_t v6off;  // payload offset of the IPv6 address block (the resident kernel re-reads it)
   uint32_t l4off;  // payload offset of the L4 header (decode<> only; the VXLAN path reads past it)

@@ -48,14 +48,15 @@ struct TileReader {
   __device__ __forceinline__ uint32_t le32(uint32_t q) const {
     const uint64_t a = (uint64_t)rel + q;
     if (a + 4 <= (uint64_t)kStage) return lds_le32(w, (uint32_t)a);
-    return slow32(q);
+    return slow32(g, gavail, q);
   }
   __device__ __forceinline__ uint32_t u8(uint32_t q) const {
     const uint64_t a = (uint64_t)rel + q;
     if (a < (uint64_t)kStage) return b[a];
     return (uint64_t)q < gavail ? g[q] : 0u;
   }
-  __device__ __noinline__ uint32_t slow32(uint32_t q) const {
+  // out of line and by value: a `this` pointer would pin the reader in scratch memory
+  static __device__ __noinline__ uint32_t slow32(const uint8_t *g, uint64_t gavail, uint32_t q) {
     uint32_t v = 0;
     for (int i = 0; i < 4; ++i) {
       const uint64_t k = (uint64_t)q + i;

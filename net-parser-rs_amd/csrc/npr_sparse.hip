@@ -351,8 +351,10 @@ __device__ __forceinline__ uint64_t lane_walk(const ParseParams &kp, uint32_t *r
 
 // a flow row as k_sparse_rows writes it (IPv6: word 0 holds the address block's payload offset)
 __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 &r0, u32x4 &r1) {
-  const bool v6 = (f.d[6] & (NPR_FLOW_KIND_IPV6 << 16)) != 0;
-  r0 = u32x4{v6 ? f.v6off : f.d[0], f.d[1], f.d[2], f.d[3]};
+  // a mask, not `v6 ? f.v6off : f.d[0]`: that select became a select of the two field addresses,
+  // which kept the whole FlowWords in scratch memory (80-B private segment)
+  const uint32_t m = 0u - ((f.d[6] >> 16) & NPR_FLOW_KIND_IPV6);
+  r0 = u32x4{(f.v6off & m) | (f.d[0] & ~m), f.d[1], f.d[2], f.d[3]};
   r1 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
 }
 // every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
