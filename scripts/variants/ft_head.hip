@@ -27,26 +27,24 @@ constexpr int kB = 256;          // threads per workgroup
 constexpr int kAggItems = 1024;  // rows per compaction block
 
 struct Key {
-  uint32_t w[10];  // kind, ports, src ip, dst ip (IPv4: one word each, the rest 0; IPv6: four each)
-  bool v6;
+  uint32_t w[11];  // kind, ports, src ip (1 or 4 words), dst ip (1 or 4 words)
+  uint32_t nw;
 };
 
-// the flow row's 5-tuple (+ family / protocol bits); IPv6 addresses from the side row.  Fixed-size
-// and fully unrolled (a loop over a run-time word count put two keys in scratch memory).
+// the flow row's 5-tuple (+ family / protocol bits); IPv6 addresses from the side row
 __device__ __forceinline__ Key row_key(const uint32_t *row, const uint32_t *v6row) {
   Key k;
   const uint32_t kind = (row[6] >> 16) & 0xffu;
   k.w[0] = kind;
   k.w[1] = row[2];  // src port | dst port << 16
-  k.v6 = (kind & NPR_FLOW_KIND_IPV6) != 0;
-  if (k.v6) {
+  if (kind & NPR_FLOW_KIND_IPV6) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) k.w[2 + i] = v6row ? v6row[i] : 0u;
+    k.nw = 10;
   } else {
     k.w[2] = row[0];
     k.w[3] = row[1];
-#pragma unroll
-    for (int i = 4; i < 10; ++i) k.w[i] = 0u;
+    k.nw = 4;
   }
   return k;
 }
@@ -60,154 +58,82 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
   return x;
 }
 
-// the first 4 words (IPv4) or all 10 (IPv6)
 __device__ __forceinline__ uint64_t key_hash(const Key &k) {
   uint64_t h = 0x9e3779b97f4a7c15ull;
-#pragma unroll
-  for (uint32_t i = 0; i < 4; ++i) h = mix64(h ^ (uint64_t)k.w[i] * 0xff51afd7ed558ccdull + i);
-  if (k.v6) {
-#pragma unroll
-    for (uint32_t i = 4; i < 10; ++i) h = mix64(h ^ (uint64_t)k.w[i] * 0xff51afd7ed558ccdull + i);
-  }
+  for (uint32_t i = 0; i < k.nw; ++i) h = mix64(h ^ (uint64_t)k.w[i] * 0xff51afd7ed558ccdull + i);
   return h;
 }
 
-// w[0] holds the family bit, and IPv4 keys are zero past their fourth word.  No short circuit: an
-// early exit per word let the compiler sink each row word's load behind the previous compare
-// (serial global loads; the Zipf aggregate went 0.186 -> 0.279 ms)
 __device__ __forceinline__ bool key_eq(const Key &a, const Key &b) {
-  uint32_t diff = 0;
-#pragma unroll
-  for (int i = 0; i < 10; ++i) diff |= a.w[i] ^ b.w[i];
-  return diff == 0;
+  if (a.nw != b.nw) return false;
+  for (uint32_t i = 0; i < a.nw; ++i)
+    if (a.w[i] != b.w[i]) return false;
+  return true;
 }
 
 __device__ __forceinline__ uint64_t row_offset(const uint32_t *row) {  // 40-bit record offset
   return ((uint64_t)row[7] << 8) | (row[6] >> 24);
 }
 
-// Find (or claim) the global slot of key k (hash h) for row i: linear probing over slot words
-// {hash32 | 1, claiming row}; a slot with the same hash is compared against its claiming row's key.
-__device__ __forceinline__ uint64_t probe(const uint32_t *flows, const uint32_t *flows_v6, uint64_t *slot_word,
-                                          uint64_t mask, const Key &k, uint64_t h, uint64_t i) {
-  const uint32_t h32 = (uint32_t)(h >> 32) | 1u;  // never 0: 0 marks an empty slot
-  const uint64_t mine = ((uint64_t)h32 << 32) | (uint32_t)i;
-  uint64_t pos = h & mask;
-  for (;;) {
-    uint64_t w = __hip_atomic_load(slot_word + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (w == 0) {
-      uint64_t expect = 0;
-      if (__hip_atomic_compare_exchange_strong(slot_word + pos, &expect, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT))
-        return pos;  // claimed
-      w = expect;
-    }
-    if ((uint32_t)(w >> 32) == h32) {  // same hash: compare with the claiming row's key
-      const uint64_t j = (uint32_t)w;
-      if (key_eq(k, row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr))) return pos;
-    }
-    pos = (pos + 1) & mask;
-  }
-}
-
-// One workgroup inserts kInsRows rows in three steps:
-//  1. every row claims (or finds) the LDS entry of its 32-bit hash; the claiming row leads it;
-//  2. leaders probe the global table; the other rows compare their key with their leader's and
-//     join its entry (count sum, first-seen minimum in LDS), or, on a 32-bit hash collision inside
-//     the workgroup, probe the global table themselves and fold straight into it;
-//  3. leaders publish their slot in the entry, joiners take it, and each entry costs one pair of
-//     global atomics.
-// So a popular flow costs one global probe per workgroup, not one per row: with one probe per row,
-// a Zipf mix's hottest slots took a CAS from every row that saw them empty at the start (all
-// workgroups are resident at once) and every later row's read on one L2 channel.  512 rows per
-// workgroup (24-KB LDS tables): 1024 measured the same on the Zipf mix but 12 % slower all-distinct
-// (48 KB, 3 workgroups per CU).
-constexpr int kInsPer = 2, kInsRows = kB * kInsPer, kLdsSlots = 2 * kInsRows;
+// One workgroup inserts kInsRows rows: each finds (or claims) its slot in the global table, then
+// the workgroup folds its rows per slot in an LDS table (count sum, first-seen minimum), so a
+// popular flow costs one pair of global atomics per workgroup, not one per row.
+constexpr int kInsPer = 4, kInsRows = kB * kInsPer, kLdsSlots = 2 * kInsRows;
 
 __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const uint32_t *flows_v6,
                                                    const uint64_t *weights, uint64_t n, uint64_t *slot_word,
                                                    uint64_t *slot_first, uint64_t *slot_count, uint32_t *slot_of_row,
                                                    uint64_t mask) {
-  __shared__ uint32_t lhash[kLdsSlots];  // the entry's hash32 (0: empty)
-  __shared__ uint32_t llead[kLdsSlots];  // the leader's row in the workgroup, then (step 3) its slot
+  __shared__ uint32_t lkey[kLdsSlots];
   __shared__ unsigned long long lcnt[kLdsSlots], lfirst[kLdsSlots];
   for (int e = threadIdx.x; e < kLdsSlots; e += kB) {
-    lhash[e] = 0;
+    lkey[e] = ~0u;
     lcnt[e] = 0;
     lfirst[e] = ~0ull;
   }
   __syncthreads();
-  const uint64_t base = (uint64_t)blockIdx.x * kInsRows;
-  Key k[kInsPer];
-  uint64_t h[kInsPer];
-  uint32_t ent[kInsPer];
-  uint32_t lead = 0, join = 0;  // bit q: row q leads / joined its entry
-#pragma unroll
   for (int q = 0; q < kInsPer; ++q) {
-    const uint32_t r = (uint32_t)q * kB + threadIdx.x;
-    const uint64_t i = base + r;
-    ent[q] = 0;
-    h[q] = 0;
-    if (i >= n) continue;
-    k[q] = row_key(flows + i * 8, flows_v6 ? flows_v6 + i * 8 : nullptr);
-    h[q] = key_hash(k[q]);
-    const uint32_t h32 = (uint32_t)(h[q] >> 32) | 1u;
-    uint32_t e = (uint32_t)h[q] & (kLdsSlots - 1);
-    for (;;) {
-      const uint32_t old = atomicCAS(&lhash[e], 0u, h32);
-      if (old == 0u) {
-        llead[e] = r;
-        lead |= 1u << q;
-        break;
-      }
-      if (old == h32) break;
-      e = (e + 1) & (kLdsSlots - 1);
-    }
-    ent[q] = e;
-  }
-  __syncthreads();
-  uint32_t pos[kInsPer];
-#pragma unroll
-  for (int q = 0; q < kInsPer; ++q) {
-    const uint64_t i = base + (uint32_t)q * kB + threadIdx.x;
-    pos[q] = 0;
+    const uint64_t i = (uint64_t)blockIdx.x * kInsRows + (uint64_t)q * kB + threadIdx.x;
     if (i >= n) continue;
     const uint32_t *row = flows + i * 8;
-    const bool ld = (lead >> q) & 1u;
-    bool jn = false;
-    if (!ld) {
-      const uint64_t j = base + llead[ent[q]];
-      jn = key_eq(k[q], row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr));
-    }
-    const unsigned long long wt = weights ? weights[i] : 1ull, off = row_offset(row);
-    if (ld || jn) {
-      if (ld) {
-        pos[q] = (uint32_t)probe(flows, flows_v6, slot_word, mask, k[q], h[q], i);
-        slot_of_row[i] = pos[q];
+    const Key k = row_key(row, flows_v6 ? flows_v6 + i * 8 : nullptr);
+    const uint64_t h = key_hash(k);
+    const uint32_t h32 = (uint32_t)(h >> 32) | 1u;  // never 0: 0 marks an empty slot
+    const uint64_t mine = ((uint64_t)h32 << 32) | (uint32_t)i;
+    uint64_t pos = h & mask;
+    for (;;) {
+      uint64_t w = __hip_atomic_load(slot_word + pos, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (w == 0) {
+        uint64_t expect = 0;
+        if (__hip_atomic_compare_exchange_strong(slot_word + pos, &expect, mine, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT))
+          break;  // claimed
+        w = expect;
       }
-      join |= (uint32_t)jn << q;
-      atomicAdd(&lcnt[ent[q]], wt);
-      atomicMin(&lfirst[ent[q]], off);
-    } else {  // a different key with the same 32-bit hash inside the workgroup
-      const uint32_t p = (uint32_t)probe(flows, flows_v6, slot_word, mask, k[q], h[q], i);
-      slot_of_row[i] = p;
-      atomicAdd((unsigned long long *)(slot_count + p), wt);
-      atomicMin((unsigned long long *)(slot_first + p), off);
+      if ((uint32_t)(w >> 32) == h32) {  // same hash: compare with the claiming row's key
+        const uint64_t j = (uint32_t)w;
+        const Key o = row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr);
+        if (key_eq(k, o)) break;
+      }
+      pos = (pos + 1) & mask;
     }
+    slot_of_row[i] = (uint32_t)pos;
+    // fold into the workgroup's LDS table (at most kInsRows distinct slots in 2x as many entries)
+    uint32_t e = (uint32_t)mix64(pos) & (kLdsSlots - 1);
+    for (;;) {
+      const uint32_t old = atomicCAS(&lkey[e], ~0u, (uint32_t)pos);
+      if (old == ~0u || old == (uint32_t)pos) break;
+      e = (e + 1) & (kLdsSlots - 1);
+    }
+    atomicAdd(&lcnt[e], (unsigned long long)(weights ? weights[i] : 1ull));
+    atomicMin(&lfirst[e], (unsigned long long)row_offset(row));
   }
   __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kInsPer; ++q)
-    if ((lead >> q) & 1u) llead[ent[q]] = pos[q];
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kInsPer; ++q)
-    if ((join >> q) & 1u) slot_of_row[base + (uint32_t)q * kB + threadIdx.x] = llead[ent[q]];
   for (int e = threadIdx.x; e < kLdsSlots; e += kB) {
-    if (lhash[e] == 0u) continue;
-    const uint32_t p = llead[e];
-    atomicAdd((unsigned long long *)(slot_count + p), lcnt[e]);
-    atomicMin((unsigned long long *)(slot_first + p), lfirst[e]);
+    const uint32_t pos = lkey[e];
+    if (pos == ~0u) continue;
+    atomicAdd((unsigned long long *)(slot_count + pos), lcnt[e]);
+    atomicMin((unsigned long long *)(slot_first + pos), lfirst[e]);
   }
 }
 

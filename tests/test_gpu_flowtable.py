@@ -133,3 +133,52 @@ def test_row_cap_is_rejected():
     fl = torch.zeros(64, dtype=torch.uint8, device="cuda")
     with pytest.raises(Exception):
         device.dev_flow_aggregate(fl, None, n=(1 << 30) + 1, cap=0)
+
+
+# ---- k_agg_insert's workgroup dedupe: rows of different keys whose 32-bit hashes collide ----------
+def _mix64(x):
+    x = x ^ (x >> np.uint64(30))
+    x = x * np.uint64(0xBF58476D1CE4E5B9)
+    x = x ^ (x >> np.uint64(27))
+    x = x * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _key_h32(words):
+    """npr_flowtable.hip key_hash over IPv4 keys {kind, ports, src ip, dst ip}: (hash >> 32) | 1."""
+    h = np.full(len(words), 0x9E3779B97F4A7C15, np.uint64)
+    for i in range(4):
+        h = _mix64(h ^ (words[:, i].astype(np.uint64) * np.uint64(0xFF51AFD7ED558CCD) + np.uint64(i)))
+    return (h >> np.uint64(32)) | np.uint64(1)
+
+
+def test_hash32_collisions_inside_a_workgroup():
+    rng = np.random.default_rng(21)
+    m = 400_000  # ~19 expected pairs of equal 32-bit hashes among m random keys
+    words = np.zeros((m, 4), np.uint32)
+    words[:, 0] = rng.choice([0, _abi.KIND_UDP], m)
+    words[:, 1:] = rng.integers(0, 2**32, (m, 3), dtype=np.uint32)
+    h32 = _key_h32(words)
+    order = np.argsort(h32, kind="stable")
+    dup = np.nonzero(h32[order][1:] == h32[order][:-1])[0]
+    pairs = [(order[d], order[d + 1]) for d in dup if (words[order[d]] != words[order[d + 1]]).any()]
+    assert len(pairs) >= 4
+    # each pair's two keys several times inside one 1024-row block (either may lead its LDS entry),
+    # among distinct filler rows
+    keys = []
+    for a, b in pairs[:8]:
+        blk = [a, b, a, a, b] if len(keys) % 2 == 0 else [b, a, b]
+        keys += list(rng.permutation(blk)) + list(rng.integers(0, m, 40))
+    keys = np.array(keys + list(rng.integers(0, m, 5000)))
+    n = len(keys)
+    rows = np.zeros(n, _abi.FLOW_DTYPE)
+    raw = rows.view(np.uint32).reshape(n, 8)
+    raw[:, 0], raw[:, 1], raw[:, 2] = words[keys, 2], words[keys, 3], words[keys, 1]
+    raw[:, 3:6] = rng.integers(0, 2**32, (n, 3), dtype=np.uint32)  # vlan / MACs: not part of the key
+    off = 24 + 64 * rng.permutation(n).astype(np.uint64)  # first-seen is not row order
+    raw[:, 6] = (raw[:, 6] & 0xFFFF) | (words[keys, 0] << 16) | ((off & 0xFF).astype(np.uint32) << 24)
+    raw[:, 7] = (off >> np.uint64(8)).astype(np.uint32)
+    fl = torch.from_numpy(rows.view(np.uint8).copy()).cuda()
+    check(fl, None, n)
+    w = torch.from_numpy(rng.integers(1, 1000, n).astype(np.int64)).cuda()
+    check(fl, None, n, weights=w)
