@@ -25,6 +25,7 @@ namespace {
 
 constexpr int kB = 256;          // threads per workgroup
 constexpr int kAggItems = 1024;  // rows per compaction block
+constexpr int kPackBits = 24;    // row bits beside the 40-bit record offset in a packed first-seen word
 
 struct Key {
   uint32_t w[10];  // kind, ports, src ip, dst ip (IPv4: one word each, the rest 0; IPv6: four each)
@@ -127,7 +128,7 @@ constexpr int kInsPer = 2, kInsRows = kB * kInsPer, kLdsSlots = 2 * kInsRows;
 __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const uint32_t *flows_v6,
                                                    const uint64_t *weights, uint64_t n, uint64_t *slot_word,
                                                    uint64_t *slot_first, uint64_t *slot_count, uint32_t *slot_of_row,
-                                                   uint64_t mask) {
+                                                   uint64_t mask, bool packed) {
   __shared__ uint32_t lhash[kLdsSlots];  // the entry's hash32 (0: empty)
   __shared__ uint32_t llead[kLdsSlots];  // the leader's row in the workgroup, then (step 3) its slot
   __shared__ unsigned long long lcnt[kLdsSlots], lfirst[kLdsSlots];
@@ -179,7 +180,8 @@ __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const 
       const uint64_t j = base + llead[ent[q]];
       jn = key_eq(k[q], row_key(flows + j * 8, flows_v6 ? flows_v6 + j * 8 : nullptr));
     }
-    const unsigned long long wt = weights ? weights[i] : 1ull, off = row_offset(row);
+    const unsigned long long wt = weights ? weights[i] : 1ull;
+    const unsigned long long off = packed ? (row_offset(row) << kPackBits) | i : row_offset(row);
     if (ld || jn) {
       if (ld) {
         pos[q] = (uint32_t)probe(flows, flows_v6, slot_word, mask, k[q], h[q], i);
@@ -213,9 +215,10 @@ __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const 
 
 // Ties: several rows of one slot may carry the slot's first-seen offset (a record listed twice,
 // or tables of several captures merged: every capture's first record sits at offset 24).  The
-// slot's first-seen ROW is the lowest row index among them (the input order the output keeps):
-// one atomic min per tied row into the slot's word, which the insert no longer needs (its claims
-// are done), reset to ~0 in between.
+// slot's first-seen ROW is the lowest row index among them (the input order the output keeps).
+// Up to 2^24 rows the packed minimum of the insert settles it; beyond, this pass: one atomic min
+// per tied row into the slot's word, which the insert no longer needs (its claims are done), reset
+// to ~0 in between.
 __global__ __launch_bounds__(kB) void k_agg_tie(const uint32_t *flows, const uint32_t *slot_of_row,
                                                 const uint64_t *slot_first, uint64_t n, uint64_t *slot_row) {
   const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
@@ -225,18 +228,19 @@ __global__ __launch_bounds__(kB) void k_agg_tie(const uint32_t *flows, const uin
 }
 
 // is row i its slot's first-seen row?
-__device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t i) {
-  return slot_row[slot_of_row[i]] == i;
+__device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask,
+                                         uint64_t i) {
+  return (slot_row[slot_of_row[i]] & rmask) == i;
 }
 
-__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t n,
+__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask, uint64_t n,
                                                   uint32_t *block_counts) {
   __shared__ uint32_t sc[kB / 64];
   const uint64_t b0 = (uint64_t)blockIdx.x * kAggItems;
   uint32_t c = 0;
   for (int k = 0; k < kAggItems / kB; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    c += (i < n && is_first(slot_of_row, slot_row, i)) ? 1u : 0u;
+    c += (i < n && is_first(slot_of_row, slot_row, rmask, i)) ? 1u : 0u;
   }
   for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
   if ((threadIdx.x & 63u) == 0) sc[threadIdx.x >> 6] = c;
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(kB) void k_agg_scan(uint32_t *counts, uint64_t nb, 
 }
 
 __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const uint32_t *flows_v6,
-                                                    const uint32_t *slot_of_row, const uint64_t *slot_row,
+                                                    const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask,
                                                     const uint64_t *slot_count, uint64_t n, const uint32_t *offsets,
                                                     uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap) {
   __shared__ uint32_t sc[kAggItems / kB][kB / 64];
@@ -277,7 +281,7 @@ __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const
 #pragma unroll
   for (int k = 0; k < kAggItems / kB; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    first[k] = i < n && is_first(slot_of_row, slot_row, i);
+    first[k] = i < n && is_first(slot_of_row, slot_row, rmask, i);
     const uint64_t bal = __ballot(first[k]);
     if (lane == 0) sc[k][wave] = (uint32_t)__builtin_popcountll(bal);
   }
@@ -336,15 +340,22 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
   if ((e = hipMemsetAsync(slot_word, 0, S * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(slot_first, 0xff, S * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(slot_count, 0, S * 8, s)) != hipSuccess) return e;
+  // up to 2^24 rows the first-seen minimum runs over {offset, row} packed in one word: ties settle
+  // inside it and the first-seen row is its low bits; beyond, a second pass settles ties
+  const bool packed = n <= (1ull << kPackBits);
   hipLaunchKernelGGL(k_agg_insert, dim3((uint32_t)((n + kInsRows - 1) / kInsRows)), dim3(kB), 0, s, flows, flows_v6, weights, n,
-                     slot_word, slot_first, slot_count, slot_of_row, S - 1);
-  uint64_t *slot_row = slot_word;  // the claims are done: the word now holds the first-seen row
-  if ((e = hipMemsetAsync(slot_row, 0xff, S * 8, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_agg_tie, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, slot_of_row, slot_first, n,
-                     slot_row);
-  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, n, block);
+                     slot_word, slot_first, slot_count, slot_of_row, S - 1, packed);
+  uint64_t *slot_row = slot_first, rmask = (1ull << kPackBits) - 1;
+  if (!packed) {
+    slot_row = slot_word;  // the claims are done: the word now holds the first-seen row
+    rmask = ~0ull;
+    if ((e = hipMemsetAsync(slot_row, 0xff, S * 8, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_agg_tie, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, slot_of_row, slot_first, n,
+                       slot_row);
+  }
+  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, rmask, n, block);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(kB), 0, s, block, nb, total);
-  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, slot_row,
+  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, slot_row, rmask,
                      slot_count, n, block, out, out_v6, counts, cap);
   return hipGetLastError();
 }

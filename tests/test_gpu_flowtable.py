@@ -182,3 +182,27 @@ def test_hash32_collisions_inside_a_workgroup():
     check(fl, None, n)
     w = torch.from_numpy(rng.integers(1, 1000, n).astype(np.int64)).cuda()
     check(fl, None, n, weights=w)
+
+
+@pytest.mark.parametrize("reps", [3, 16385])
+def test_tiled_table_every_flow_tied(reps):
+    """A 1024-row table repeated: every copy of a row carries the same record offset, so each flow's
+    first-seen row is decided by the tie rule (lowest row: the first copy).  reps * 1024 > 2^24 runs
+    the two-pass tie path (k_agg_tie); below that the packed {offset, row} minimum settles it."""
+    blob = synth.flow_mix(1500, n_flows=300, seed=5)
+    fl, f6, n = device_table(blob)
+    t = 1024
+    assert n >= t
+    flows = fl[: t * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+    v6 = f6[: t * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
+    rows, counts = _flowtable_ref.aggregate(flows, v6, None)
+    big, big6 = fl[: t * 32].repeat(reps), f6[: t * 32].repeat(reps)
+    out, out6, cnt, n_out = device.dev_flow_aggregate(big, big6, n=t * reps)
+    torch.cuda.synchronize()
+    k = int(n_out.item())
+    assert k == len(rows)
+    assert out[: k * 32].cpu().numpy().tobytes() == flows[rows].tobytes()
+    assert out6[: k * 32].cpu().numpy().tobytes() == v6[rows].tobytes()
+    assert np.array_equal(cnt[:k].cpu().numpy().astype(np.uint64), counts.astype(np.uint64) * np.uint64(reps))
+    del big, big6, out, out6, cnt
+    torch.cuda.empty_cache()
