@@ -233,17 +233,25 @@ __device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint
   return (slot_row[slot_of_row[i]] & rmask) == i;
 }
 
+// Block counts of first-seen rows, and the first-seen flags themselves as one 64-bit mask per wave
+// and round (kMaskWords per block), so the scatter reads 128 B per block instead of a random slot
+// word per row.
+constexpr int kRounds = kAggItems / kB, kMaskWords = kAggItems / 64;
+static_assert(kB == 256, "the scatter sums four waves' masks");
 __global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask, uint64_t n,
-                                                  uint32_t *block_counts) {
+                                                  uint32_t *block_counts, uint64_t *first_bits) {
   __shared__ uint32_t sc[kB / 64];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t b0 = (uint64_t)blockIdx.x * kAggItems;
   uint32_t c = 0;
-  for (int k = 0; k < kAggItems / kB; ++k) {
+#pragma unroll
+  for (int k = 0; k < kRounds; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    c += (i < n && is_first(slot_of_row, slot_row, rmask, i)) ? 1u : 0u;
+    const uint64_t bal = __ballot(i < n && is_first(slot_of_row, slot_row, rmask, i));
+    if (lane == 0) first_bits[(uint64_t)blockIdx.x * kMaskWords + k * (kB / 64) + wave] = bal;
+    c += (uint32_t)__builtin_popcountll(bal);
   }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
-  if ((threadIdx.x & 63u) == 0) sc[threadIdx.x >> 6] = c;
+  if (lane == 0) sc[wave] = c;
   __syncthreads();
   if (threadIdx.x == 0) block_counts[blockIdx.x] = sc[0] + sc[1] + sc[2] + sc[3];
 }
@@ -271,29 +279,23 @@ __global__ __launch_bounds__(kB) void k_agg_scan(uint32_t *counts, uint64_t nb, 
 }
 
 __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const uint32_t *flows_v6,
-                                                    const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask,
+                                                    const uint32_t *slot_of_row, const uint64_t *first_bits,
                                                     const uint64_t *slot_count, uint64_t n, const uint32_t *offsets,
                                                     uint32_t *out, uint32_t *out_v6, uint64_t *counts, uint64_t cap) {
-  __shared__ uint32_t sc[kAggItems / kB][kB / 64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint64_t b0 = (uint64_t)blockIdx.x * kAggItems;
-  bool first[kAggItems / kB];
-#pragma unroll
-  for (int k = 0; k < kAggItems / kB; ++k) {
-    const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    first[k] = i < n && is_first(slot_of_row, slot_row, rmask, i);
-    const uint64_t bal = __ballot(first[k]);
-    if (lane == 0) sc[k][wave] = (uint32_t)__builtin_popcountll(bal);
-  }
-  __syncthreads();
+  const uint64_t *fb = first_bits + (uint64_t)blockIdx.x * kMaskWords;  // uniform: scalar loads
   uint64_t base = offsets[blockIdx.x];
 #pragma unroll
-  for (int k = 0; k < kAggItems / kB; ++k) {
+  for (int k = 0; k < kRounds; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    const uint64_t bal = __ballot(first[k]);
-    if (first[k]) {
+    const uint64_t m0 = fb[k * 4], m1 = fb[k * 4 + 1], m2 = fb[k * 4 + 2], m3 = fb[k * 4 + 3];
+    const uint32_t c0 = (uint32_t)__builtin_popcountll(m0), c1 = (uint32_t)__builtin_popcountll(m1),
+                   c2 = (uint32_t)__builtin_popcountll(m2);
+    const uint64_t bal = wave == 0 ? m0 : wave == 1 ? m1 : wave == 2 ? m2 : m3;
+    if ((bal >> lane) & 1ull) {
       uint64_t r = base + (uint64_t)__builtin_popcountll(bal & ((1ull << lane) - 1ull));
-      for (uint32_t w = 0; w < wave; ++w) r += sc[k][w];
+      r += (wave > 0 ? c0 : 0u) + (wave > 1 ? c1 : 0u) + (wave > 2 ? c2 : 0u);
       if (r < cap) {
         const uint4 *src = reinterpret_cast<const uint4 *>(flows + i * 8);
         uint4 *dst = reinterpret_cast<uint4 *>(out + r * 8);
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(kB) void k_agg_scatter(const uint32_t *flows, const
         if (counts) counts[r] = slot_count[slot_of_row[i]];
       }
     }
-    base += sc[k][0] + sc[k][1] + sc[k][2] + sc[k][3];
+    base += c0 + c1 + c2 + (uint32_t)__builtin_popcountll(m3);
   }
 }
 
@@ -325,7 +327,7 @@ uint64_t flow_table_slots(uint64_t n) {  // n <= kMaxAggRows: S <= 2^31, so a sl
 }
 uint64_t flow_table_bytes(uint64_t n) {
   const uint64_t s = flow_table_slots(n), nb = (n + kAggItems - 1) / kAggItems;
-  return s * 24 + n * 4 + nb * 4 + 64;
+  return s * 24 + n * 4 + nb * 4 + nb * kMaskWords * 8 + 64;
 }
 
 hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6, const uint64_t *weights, uint64_t n,
@@ -335,7 +337,8 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
   if (n > kMaxAggRows) return hipErrorInvalidValue;  // slot indices are 32-bit, ~0 marks an empty LDS entry
   const uint64_t S = flow_table_slots(n), nb = (n + kAggItems - 1) / kAggItems;
   uint64_t *slot_word = (uint64_t *)work, *slot_first = slot_word + S, *slot_count = slot_first + S;
-  uint32_t *slot_of_row = (uint32_t *)(slot_count + S), *block = slot_of_row + n;
+  uint64_t *first_bits = slot_count + S;
+  uint32_t *slot_of_row = (uint32_t *)(first_bits + nb * kMaskWords), *block = slot_of_row + n;
   hipError_t e;
   if ((e = hipMemsetAsync(slot_word, 0, S * 8, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(slot_first, 0xff, S * 8, s)) != hipSuccess) return e;
@@ -353,9 +356,9 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
     hipLaunchKernelGGL(k_agg_tie, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, slot_of_row, slot_first, n,
                        slot_row);
   }
-  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, rmask, n, block);
+  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, rmask, n, block, first_bits);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(kB), 0, s, block, nb, total);
-  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, slot_row, rmask,
+  hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, first_bits,
                      slot_count, n, block, out, out_v6, counts, cap);
   return hipGetLastError();
 }
