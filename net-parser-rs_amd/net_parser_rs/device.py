@@ -15,6 +15,36 @@ import torch
 
 from . import _abi, context
 
+_side_streams = {}
+
+
+class _On:
+    """The stream a call launches on.  The caller's stream when it has a handle; torch's default
+    stream is the null stream, which the C-ABI cannot name (NULL selects the context's own
+    non-blocking stream, unordered with the null stream), so then a side stream fenced to it on
+    both sides: it waits for the default stream's earlier work, and the default stream waits for
+    the call (exit)."""
+
+    def __init__(self, dev, stream):
+        dev = torch.device(dev)
+        self.user = stream if stream is not None else torch.cuda.current_stream(dev)
+        self.s = self.user
+        if self.user.cuda_stream == 0:
+            key = dev.index or 0
+            if key not in _side_streams:
+                _side_streams[key] = torch.cuda.Stream(device=dev)
+            self.s = _side_streams[key]
+            self.s.wait_stream(self.user)
+
+    def __enter__(self):
+        return self.s
+
+    def __exit__(self, *exc):
+        if self.s is not self.user:
+            self.user.wait_stream(self.s)
+        return False
+
+
 
 class Workspace:
     def __init__(self, record_cap, flow_cap, device=0, records=True, offsets=False, status=False,
@@ -37,9 +67,9 @@ class Workspace:
     def launch(self, buf, start=24, endianness=_abi.LITTLE, nbytes=None, stream=None):
         assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
         n = buf.numel() if nbytes is None else int(nbytes)
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        st = self.ctx.lib.npr_dev_parse_extract(self.ctx.handle, buf.data_ptr(), n, start, endianness,
-                                                ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        with _On(self.device, stream) as s:
+            st = self.ctx.lib.npr_dev_parse_extract(self.ctx.handle, buf.data_ptr(), n, start, endianness,
+                                                    ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
 
@@ -55,11 +85,11 @@ class Workspace:
         first record at/after it is speculated and reported as summary.entry."""
         assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
         n = buf.numel() if nbytes is None else int(nbytes)
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
         ref = _abi.NO_ENTRY if ref_record is None else int(ref_record)
-        st = self.ctx.lib.npr_dev_parse_extract_range(self.ctx.handle, buf.data_ptr(), n, int(start), int(stop),
-                                                      endianness, 1 if speculative else 0, ref,
-                                                      ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        with _On(self.device, stream) as s:
+            st = self.ctx.lib.npr_dev_parse_extract_range(self.ctx.handle, buf.data_ptr(), n, int(start), int(stop),
+                                                          endianness, 1 if speculative else 0, ref,
+                                                          ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
 
@@ -68,10 +98,10 @@ class Workspace:
         one launch per chunk, no host synchronisation, same outputs as launch()."""
         assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
         n = buf.numel() if nbytes is None else int(nbytes)
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
-        st = self.ctx.lib.npr_dev_parse_extract_chunked(self.ctx.handle, buf.data_ptr(), n, int(start), endianness,
-                                                        ctypes.byref(self.outs), int(chunk_bytes),
-                                                        ctypes.c_void_p(s.cuda_stream))
+        with _On(self.device, stream) as s:
+            st = self.ctx.lib.npr_dev_parse_extract_chunked(self.ctx.handle, buf.data_ptr(), n, int(start), endianness,
+                                                            ctypes.byref(self.outs), int(chunk_bytes),
+                                                            ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
 
@@ -82,11 +112,11 @@ class Workspace:
         usec_magic / ts_ref: the capture's speculation context (its buffer lacks the header)."""
         assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
         n = buf.numel() if nbytes is None else int(nbytes)
-        s = stream if stream is not None else torch.cuda.current_stream(self.device)
         sh = _abi.ShardC(int(base), int(start), int(stop), 1 if speculative else 0, 1 if usec_magic else 0,
                          _abi.NO_ENTRY if ts_ref is None else int(ts_ref), int(chunk_bytes))
-        st = self.ctx.lib.npr_dev_parse_extract_shard(self.ctx.handle, buf.data_ptr(), n, endianness, ctypes.byref(sh),
-                                                      ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
+        with _On(self.device, stream) as s:
+            st = self.ctx.lib.npr_dev_parse_extract_shard(self.ctx.handle, buf.data_ptr(), n, endianness, ctypes.byref(sh),
+                                                          ctypes.byref(self.outs), ctypes.c_void_p(s.cuda_stream))
         self.ctx.check(st)
         self._stream = s
 
@@ -145,13 +175,13 @@ def launch_batch(items, ctx=None, stream=None):
     if not items:
         return
     ctx = ctx if ctx is not None else items[0][0].ctx
-    s = stream if stream is not None else torch.cuda.current_stream(items[0][1].device)
     arr = (_abi.BatchItemC * len(items))()
     for i, (ws, buf, start, e) in enumerate(items):
         assert buf.is_cuda and buf.dtype == torch.uint8 and buf.is_contiguous()
         arr[i] = _abi.BatchItemC(buf.data_ptr(), buf.numel(), int(start), int(e), 0, ws.outs)
-    ctx.check(ctx.lib.npr_dev_parse_extract_batch(ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(items),
-                                                   ctypes.c_void_p(s.cuda_stream)))
+    with _On(items[0][1].device, stream) as s:
+        ctx.check(ctx.lib.npr_dev_parse_extract_batch(ctx.handle, ctypes.cast(arr, ctypes.c_void_p), len(items),
+                                                       ctypes.c_void_p(s.cuda_stream)))
     for ws, *_ in items:
         ws._stream = s
 
@@ -204,10 +234,10 @@ def dev_extract_flows(buf, recs, flows=None, flows_v6=None, status=None, ctx=Non
     flows_v6 = mk(n * 32) if flows_v6 is None else flows_v6
     status = mk(n) if status is None else status
     ctx = ctx if ctx is not None else context(dev.index or 0)
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
-    ctx.check(ctx.lib.npr_dev_extract_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
-                                            flows.data_ptr(), flows_v6.data_ptr(), status.data_ptr(),
-                                            ctypes.c_void_p(s.cuda_stream)))
+    with _On(dev, stream) as s:
+        ctx.check(ctx.lib.npr_dev_extract_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
+                                                flows.data_ptr(), flows_v6.data_ptr(), status.data_ptr(),
+                                                ctypes.c_void_p(s.cuda_stream)))
     return flows, flows_v6, status
 
 
@@ -227,11 +257,11 @@ def dev_flow_aggregate(flows, flows_v6=None, n=None, weights=None, cap=None, ctx
     if weights is not None:
         assert weights.is_cuda and weights.dtype == torch.int64 and weights.numel() >= n
     ctx = ctx if ctx is not None else context(dev.index or 0)
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
     p = lambda t: t.data_ptr() if t is not None else None
-    ctx.check(ctx.lib.npr_dev_flow_aggregate(ctx.handle, flows.data_ptr(), p(flows_v6), p(weights), n, out.data_ptr(),
-                                             out_v6.data_ptr(), counts.data_ptr(), cap, n_out.data_ptr(),
-                                             ctypes.c_void_p(s.cuda_stream)))
+    with _On(dev, stream) as s:
+        ctx.check(ctx.lib.npr_dev_flow_aggregate(ctx.handle, flows.data_ptr(), p(flows_v6), p(weights), n,
+                                                 out.data_ptr(), out_v6.data_ptr(), counts.data_ptr(), cap,
+                                                 n_out.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
     return out, out_v6, counts, n_out
 
 
@@ -243,10 +273,11 @@ def dev_vxlan_flows(buf, recs, dst_port=0, big=True, ctx=None, stream=None):
     mk = lambda nbytes: torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=dev)
     flows, flows_v6, status, vni = mk(n * 32), mk(n * 32), mk(n), mk(n * 4)
     ctx = ctx if ctx is not None else context(dev.index or 0)
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
-    ctx.check(ctx.lib.npr_dev_vxlan_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n, int(dst_port),
-                                          _abi.BIG if big else _abi.LITTLE, flows.data_ptr(), flows_v6.data_ptr(),
-                                          status.data_ptr(), vni.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    with _On(dev, stream) as s:
+        ctx.check(ctx.lib.npr_dev_vxlan_flows(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
+                                              int(dst_port), _abi.BIG if big else _abi.LITTLE, flows.data_ptr(),
+                                              flows_v6.data_ptr(), status.data_ptr(), vni.data_ptr(),
+                                              ctypes.c_void_p(s.cuda_stream)))
     return flows, flows_v6, status, vni
 
 
@@ -262,10 +293,10 @@ def dev_convert_records(buf, recs, cap=None, out=None, out_v6=None, with_v6=True
     out_v6 = (mk(cap * 32) if out_v6 is None else out_v6) if with_v6 else None
     n_out = torch.zeros(1, dtype=torch.int64, device=dev)
     ctx = ctx if ctx is not None else context(dev.index or 0)
-    s = stream if stream is not None else torch.cuda.current_stream(dev)
-    ctx.check(ctx.lib.npr_dev_convert_records(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
-                                              out.data_ptr(), out_v6.data_ptr() if out_v6 is not None else None,
-                                              cap, n_out.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
+    with _On(dev, stream) as s:
+        ctx.check(ctx.lib.npr_dev_convert_records(ctx.handle, buf.data_ptr(), buf.numel(), recs.data_ptr(), n,
+                                                  out.data_ptr(), out_v6.data_ptr() if out_v6 is not None else None,
+                                                  cap, n_out.data_ptr(), ctypes.c_void_p(s.cuda_stream)))
     return out, out_v6, n_out
 
 

@@ -246,6 +246,83 @@ def gather_flows(mine: ShardResult, metas: List[ShardResult], live, group=None, 
     return f, (out6.cpu().numpy().view(_abi.FLOW_V6_DTYPE) if out6 is not None else None)
 
 
+def device_aggregate(flows, flows_v6, n, weights=None):
+    """Row f4 on this rank's GPU (npr_dev_flow_aggregate): -> (rows, rows_v6, counts, k), the first k
+    rows / side rows (uint8, 32 B each) and their int64 counts."""
+    import torch
+    from . import device
+    out, out6, cnt, n_out = device.dev_flow_aggregate(flows, flows_v6, n=n, weights=weights)
+    k = int(n_out.item())  # synchronises the stream
+    return out[: k * 32], (out6[: k * 32] if flows_v6 is not None else None), cnt[:k].to(torch.int64), k
+
+
+def gather_distinct_flows(flows, flows_v6, n, weights=None, group=None, dst=0, aggregate=device_aggregate):
+    """The distinct-flow table (row f4) of the merged convert_records table, moving only each rank's
+    distinct rows (it shrinks the gather when flows repeat).  `flows` / `flows_v6`
+    are this rank's n rows (uint8 tensors, n * 32 bytes; flows_v6 for every rank or for none) in the
+    merged table's order, which puts the ranks in reverse (merged_positions); `weights` (int64) when
+    the rows are already aggregates.  Every rank aggregates its rows; the k_r distinct rows, side
+    rows and counts go to `dst` by point-to-point transfers, in reverse rank order; dst aggregates
+    them again weighted by the counts.  That is exact: a key's first-seen row (lowest record offset)
+    is in some rank's table, each rank's table keeps its first-seen rows in input order, and the
+    counts add.  Returns (rows, rows_v6, counts, k) on dst, None elsewhere.  `aggregate` is the
+    local table builder (device_aggregate; the CPU tests pass the checker)."""
+    import torch
+    import torch.distributed as dist
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rows, rows6, cnt, k = aggregate(flows, flows_v6, n, weights)
+    gloo = dist.get_backend(group) == "gloo"  # gloo moves host tensors only
+    if gloo:
+        rows, cnt = rows.cpu(), cnt.cpu()
+        rows6 = rows6.cpu() if rows6 is not None else None
+    dev = rows.device
+    mine = torch.tensor([k, 1 if flows_v6 is not None else 0], dtype=torch.int64, device=dev)
+    ks = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(ks, mine, group=group)
+    ks = [(int(t[0]), int(t[1])) for t in (x.cpu() for x in ks)]
+    if len({v for _, v in ks}) != 1:
+        raise ValueError("gather_distinct_flows: every rank passes a side table, or none does")
+    with_v6 = bool(ks[0][1])
+    gr = (lambda r: dist.get_global_rank(group, r)) if group is not None else (lambda r: r)
+    reqs = []
+    if rank != dst:
+        if k:
+            reqs.append(dist.isend(rows.contiguous(), gr(dst), group=group))
+            if with_v6:
+                reqs.append(dist.isend(rows6.contiguous(), gr(dst), group=group))
+            reqs.append(dist.isend(cnt.contiguous(), gr(dst), group=group))
+        for q in reqs:
+            q.wait()
+        return None
+    total = sum(kr for kr, _ in ks)
+    all_rows = torch.empty(max(total, 1) * 32, dtype=torch.uint8, device=dev)[: total * 32]
+    all_v6 = torch.empty(max(total, 1) * 32, dtype=torch.uint8, device=dev)[: total * 32] if with_v6 else None
+    all_cnt = torch.empty(max(total, 1), dtype=torch.int64, device=dev)[:total]
+    p = 0
+    for r in reversed(range(world)):
+        kr = ks[r][0]
+        if not kr:
+            continue
+        sl, sc = slice(p * 32, (p + kr) * 32), slice(p, p + kr)
+        if r == rank:
+            all_rows[sl].copy_(rows)
+            if with_v6:
+                all_v6[sl].copy_(rows6)
+            all_cnt[sc].copy_(cnt)
+        else:
+            reqs.append(dist.irecv(all_rows[sl], gr(r), group=group))
+            if with_v6:
+                reqs.append(dist.irecv(all_v6[sl], gr(r), group=group))
+            reqs.append(dist.irecv(all_cnt[sc], gr(r), group=group))
+        p += kr
+    for q in reqs:
+        q.wait()
+    if gloo and flows.is_cuda:  # the merge runs where the local tables were built
+        all_rows, all_cnt = all_rows.to(flows.device), all_cnt.to(flows.device)
+        all_v6 = all_v6.to(flows.device) if all_v6 is not None else None
+    return aggregate(all_rows, all_v6, total, all_cnt)
+
+
 def device_local(ws, buf, length, endianness=_abi.LITTLE, ref_record=24) -> LocalParse:
     """The product's local parser: npr_dev_parse_extract_range on this rank's GPU (`ws` a
     device.Workspace, `buf` the whole capture in HBM).  Results are copied to the host."""

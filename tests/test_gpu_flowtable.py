@@ -206,3 +206,29 @@ def test_tiled_table_every_flow_tied(reps):
     assert np.array_equal(cnt[:k].cpu().numpy().astype(np.uint64), counts.astype(np.uint64) * np.uint64(reps))
     del big, big6, out, out6, cnt
     torch.cuda.empty_cache()
+
+
+def test_distinct_flow_gather_on_the_device_world1():
+    """parallel.gather_distinct_flows with the device aggregate (world 1 over gloo: the local
+    table, the all-gather of its size, then the weighted merge on the GPU)."""
+    import socket
+    import torch.distributed as dist
+    from net_parser_rs import parallel
+    blob = synth.flow_mix(30_000, n_flows=700, seed=12)
+    fl, f6, n = device_table(blob)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        rows, rows6, cnt, k = parallel.gather_distinct_flows(fl[: n * 32], f6[: n * 32], n)
+    finally:
+        dist.destroy_process_group()
+    flows = fl[: n * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+    v6 = f6[: n * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
+    want, counts = _flowtable_ref.aggregate(flows, v6, None)
+    assert k == len(want) < n
+    assert rows.cpu().numpy().tobytes() == flows[want].tobytes()
+    assert rows6.cpu().numpy().tobytes() == v6[want].tobytes()
+    assert np.array_equal(cnt.cpu().numpy().astype(np.uint64), counts)

@@ -572,3 +572,59 @@ def test_gloo_world8_failing_rank_ends_the_others():
     assert codes[5] == 1, codes  # the injected exception
     assert all(c != 0 for c in codes), codes  # nobody finished the loop without rank 5
     assert took < 120, took
+
+
+# ---- row f4 across ranks: gather each rank's distinct flows, merge them weighted -----------------
+def cpu_aggregate(flows, flows_v6, n, weights=None):
+    """parallel.gather_distinct_flows' `aggregate` on host tensors: the row-f4 checker."""
+    import torch
+    import _flowtable_ref
+    f = flows[: n * 32].numpy().view(_abi.FLOW_DTYPE)
+    v = flows_v6[: n * 32].numpy().view(_abi.FLOW_V6_DTYPE) if flows_v6 is not None else np.zeros(n, _abi.FLOW_V6_DTYPE)
+    rows, counts = _flowtable_ref.aggregate(f, v, None if weights is None else weights[:n].numpy())
+    b = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy())
+    return b(f[rows]), (b(v[rows]) if flows_v6 is not None else None), torch.from_numpy(counts.astype(np.int64)), len(rows)
+
+
+def _distinct_main(rank, world, port, cuts, with_v6, q):
+    import torch
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        blob = synth.flow_mix(6_000, n_flows=150, seed=44)
+        _, _, recs, _ = _oracle.capture_file_parse(blob)
+        flows, v6 = _oracle.convert_records(blob, recs)
+        # the merged table's pieces in order belong to ranks world-1 ... 0 (reverse rank order)
+        edges = [0] + list(cuts) + [len(flows)]
+        j = world - 1 - rank
+        lo, hi = edges[j], edges[j + 1]
+        b = lambda a: torch.from_numpy(np.ascontiguousarray(a).view(np.uint8).reshape(-1).copy())
+        got = parallel.gather_distinct_flows(b(flows[lo:hi]), b(v6[lo:hi]) if with_v6 else None, hi - lo,
+                                             aggregate=cpu_aggregate)
+        if rank == 0:
+            want = cpu_aggregate(b(flows), b(v6) if with_v6 else None, len(flows))
+            rows, rows6, cnt, k = got
+            ok = k == want[3] and rows.numpy().tobytes() == want[0].numpy().tobytes() and \
+                bool((cnt == want[2]).all()) and (not with_v6 or rows6.numpy().tobytes() == want[1].numpy().tobytes())
+            q.put(bool(ok and 0 < k < len(flows)))
+        else:
+            assert got is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,cuts,with_v6", [(2, (2500,), True), (3, (1000, 1000), True), (3, (700, 4100), False)])
+def test_gloo_distinct_flow_gather_equals_one_aggregate(world, cuts, with_v6):
+    """Each rank aggregates its piece of the convert_records table; the root merges the gathered
+    distinct rows weighted by their counts: the same table as one aggregate of the whole (an empty
+    piece included: cuts (1000, 1000) leave rank 1 with no rows)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_distinct_main, args=(r, world, port, cuts, with_v6, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    assert q.get(timeout=10) is True
