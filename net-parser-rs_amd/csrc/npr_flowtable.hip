@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const 
       const uint32_t p = (uint32_t)probe(flows, flows_v6, slot_word, mask, k[q], h[q], i);
       slot_of_row[i] = p;
       atomicAdd((unsigned long long *)(slot_count + p), wt);
-      atomicMin((unsigned long long *)(slot_first + p), off);
+      atomicMax((unsigned long long *)(slot_first + p), ~off);
     }
   }
   __syncthreads();
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kB) void k_agg_insert(const uint32_t *flows, const 
     if (lhash[e] == 0u) continue;
     const uint32_t p = llead[e];
     atomicAdd((unsigned long long *)(slot_count + p), lcnt[e]);
-    atomicMin((unsigned long long *)(slot_first + p), lfirst[e]);
+    atomicMax((unsigned long long *)(slot_first + p), ~lfirst[e]);
   }
 }
 
@@ -224,13 +224,14 @@ __global__ __launch_bounds__(kB) void k_agg_tie(const uint32_t *flows, const uin
   const uint64_t i = (uint64_t)blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   const uint32_t pos = slot_of_row[i];
-  if (row_offset(flows + i * 8) == slot_first[pos]) atomicMin((unsigned long long *)(slot_row + pos), (unsigned long long)i);
+  if (row_offset(flows + i * 8) == ~slot_first[pos]) atomicMin((unsigned long long *)(slot_row + pos), (unsigned long long)i);
 }
 
 // is row i its slot's first-seen row?
-__device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask,
-                                         uint64_t i) {
-  return (slot_row[slot_of_row[i]] & rmask) == i;
+// slot_row ^ rxor, masked by rmask: the packed first-seen word (stored complemented) or the tie pass's row
+__device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rxor,
+                                         uint64_t rmask, uint64_t i) {
+  return ((slot_row[slot_of_row[i]] ^ rxor) & rmask) == i;
 }
 
 // Block counts of first-seen rows, and the first-seen flags themselves as one 64-bit mask per wave
@@ -238,7 +239,7 @@ __device__ __forceinline__ bool is_first(const uint32_t *slot_of_row, const uint
 // word per row.
 constexpr int kRounds = kAggItems / kB, kMaskWords = kAggItems / 64;
 static_assert(kB == 256, "the scatter sums four waves' masks");
-__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rmask, uint64_t n,
+__global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, const uint64_t *slot_row, uint64_t rxor, uint64_t rmask, uint64_t n,
                                                   uint32_t *block_counts, uint64_t *first_bits) {
   __shared__ uint32_t sc[kB / 64];
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(kB) void k_agg_count(const uint32_t *slot_of_row, c
 #pragma unroll
   for (int k = 0; k < kRounds; ++k) {
     const uint64_t i = b0 + threadIdx.x + (uint64_t)k * kB;
-    const uint64_t bal = __ballot(i < n && is_first(slot_of_row, slot_row, rmask, i));
+    const uint64_t bal = __ballot(i < n && is_first(slot_of_row, slot_row, rxor, rmask, i));
     if (lane == 0) first_bits[(uint64_t)blockIdx.x * kMaskWords + k * (kB / 64) + wave] = bal;
     c += (uint32_t)__builtin_popcountll(bal);
   }
@@ -340,23 +341,24 @@ hipError_t launch_flow_aggregate(const uint32_t *flows, const uint32_t *flows_v6
   uint64_t *first_bits = slot_count + S;
   uint32_t *slot_of_row = (uint32_t *)(first_bits + nb * kMaskWords), *block = slot_of_row + n;
   hipError_t e;
-  if ((e = hipMemsetAsync(slot_word, 0, S * 8, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(slot_first, 0xff, S * 8, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(slot_count, 0, S * 8, s)) != hipSuccess) return e;
+  // one zero fill: claim words, first-seen words (stored complemented: the minimum is an atomic max
+  // from 0) and counts are consecutive
+  if ((e = hipMemsetAsync(slot_word, 0, S * 24, s)) != hipSuccess) return e;
   // up to 2^24 rows the first-seen minimum runs over {offset, row} packed in one word: ties settle
   // inside it and the first-seen row is its low bits; beyond, a second pass settles ties
   const bool packed = n <= (1ull << kPackBits);
   hipLaunchKernelGGL(k_agg_insert, dim3((uint32_t)((n + kInsRows - 1) / kInsRows)), dim3(kB), 0, s, flows, flows_v6, weights, n,
                      slot_word, slot_first, slot_count, slot_of_row, S - 1, packed);
-  uint64_t *slot_row = slot_first, rmask = (1ull << kPackBits) - 1;
+  uint64_t *slot_row = slot_first, rxor = ~0ull, rmask = (1ull << kPackBits) - 1;
   if (!packed) {
     slot_row = slot_word;  // the claims are done: the word now holds the first-seen row
+    rxor = 0;
     rmask = ~0ull;
     if ((e = hipMemsetAsync(slot_row, 0xff, S * 8, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_agg_tie, dim3((uint32_t)((n + kB - 1) / kB)), dim3(kB), 0, s, flows, slot_of_row, slot_first, n,
                        slot_row);
   }
-  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, rmask, n, block, first_bits);
+  hipLaunchKernelGGL(k_agg_count, dim3((uint32_t)nb), dim3(kB), 0, s, slot_of_row, slot_row, rxor, rmask, n, block, first_bits);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(kB), 0, s, block, nb, total);
   hipLaunchKernelGGL(k_agg_scatter, dim3((uint32_t)nb), dim3(kB), 0, s, flows, flows_v6, slot_of_row, first_bits,
                      slot_count, n, block, out, out_v6, counts, cap);
