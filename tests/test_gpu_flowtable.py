@@ -232,3 +232,21 @@ def test_distinct_flow_gather_on_the_device_world1():
     assert rows.cpu().numpy().tobytes() == flows[want].tobytes()
     assert rows6.cpu().numpy().tobytes() == v6[want].tobytes()
     assert np.array_equal(cnt.cpu().numpy().astype(np.uint64), counts)
+
+
+@pytest.mark.parametrize("m", [1, 2, 100, 511, 512, 513, 1023, 1024, 1025])
+def test_small_tables_read_without_device_sync(m):
+    """Tables around the 512-row insert and 1024-row compaction block edges, the count read by
+    .item() on the default stream with no torch.cuda.synchronize(): the device layer fences its
+    side stream to the default stream (device._On), so the read waits for the aggregate."""
+    blob = synth.flow_mix(3_000, n_flows=400, seed=77)
+    fl, f6, n = device_table(blob)
+    assert n >= m
+    flows = fl[: m * 32].cpu().numpy().view(_abi.FLOW_DTYPE)
+    v6 = f6[: m * 32].cpu().numpy().view(_abi.FLOW_V6_DTYPE)
+    want, counts = _flowtable_ref.aggregate(flows, v6, None)
+    out, out6, cnt, n_out = device.dev_flow_aggregate(fl[: m * 32].contiguous(), f6[: m * 32].contiguous(), n=m)
+    k = int(n_out.item())
+    assert k == len(want)
+    assert out[: k * 32].cpu().numpy().tobytes() == flows[want].tobytes()
+    assert np.array_equal(cnt[:k].cpu().numpy().astype(np.uint64), counts)
