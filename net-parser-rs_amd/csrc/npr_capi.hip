@@ -221,10 +221,21 @@ npr_status probe_density(npr_ctx *c, const void *input, uint64_t start, uint64_t
   pr.sum = nullptr;
   return NPR_OK;
 }
-// The parse whose summary is `sum` chose its pass by the entry for (input, start, stop, e).
+// The parse whose summary is `sum` chose its pass by the entry for (input, start, stop, e): that
+// entry alone is corrected by what the summary reports.  A summary buffer is reused (one Workspace
+// alternating between two captures): the other entries that held it let it go, so a check of one
+// capture's parse never rewrites another capture's density.
 void probe_note(npr_ctx *c, const void *input, uint64_t start, uint64_t stop, npr_endianness e, const npr_summary *sum) {
+  for (auto &pr : c->probes) {
+    if (pr.input && pr.input == input && pr.start == start && pr.stop == stop && pr.e == (int)e) pr.sum = sum;
+    else if (pr.sum == sum) pr.sum = nullptr;
+  }
+}
+// A parse that chose by no entry (a shard, a speculative start, a record-table launch, a caller's
+// own range or chain link) writes `sum`: no entry is corrected by it.
+void probe_unbind(npr_ctx *c, const npr_summary *sum) {
   for (auto &pr : c->probes)
-    if (pr.input == input && pr.start == start && pr.stop == stop && pr.e == (int)e) pr.sum = sum;
+    if (pr.sum == sum) pr.sum = nullptr;
 }
 // Forget the density of the capture at `input` (nullptr: of every capture).
 void probe_forget(npr_ctx *c, const void *input) {
@@ -571,27 +582,6 @@ npr_status npr_record_parse(const uint8_t *in, size_t len, npr_endianness e, npr
 }
 
 // ---- device-resident hot path -----------------------------------------------------------------
-npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
-                                 npr_endianness e, const npr_dev_outputs *o, void *stream) {
-  // flows-only captures larger than one launch keeps in registers: chained chunks of that size
-  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start && input &&
-      ((uintptr_t)input & 15u) == 0) {
-    npr_status st = res_geometry(c);
-    if (st) return st;
-    uint64_t span = 0;  // long records: the sparse walk, one launch set for any size
-    if ((st = sparse_choice(c, input, start, len, e, true, stream, span))) return st;
-    probe_note(c, input, start, len, e, o->summary);
-    if (span) {
-      SpanScope scope{c};
-      c->sparse_span = span;
-      return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
-    }
-    if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
-      return npr_dev_parse_extract_chunked(c, input, len, start, e, o, 0, stream);
-  }
-  return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
-}
-
 // A shard's buffer holds file bytes [base, len) only: byte offsets stay file offsets, and the
 // speculation context (the magic's ts_usec bound, a reference ts_sec) comes from the host.
 struct ShardSpec {
@@ -605,6 +595,29 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
                                npr_endianness e, int speculative_start, uint64_t ref_record,
                                const npr_summary *prev, const npr_dev_outputs *o, void *stream,
                                const ShardSpec *sh = nullptr);
+
+npr_status npr_dev_parse_extract(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
+                                 npr_endianness e, const npr_dev_outputs *o, void *stream) {
+  // flows-only captures larger than one launch keeps in registers: chained chunks of that size
+  if (c && o && c->resident && !o->record_offsets && !o->records && !o->record_status && len > start && input &&
+      ((uintptr_t)input & 15u) == 0) {
+    npr_status st = res_geometry(c);
+    if (st) return st;
+    uint64_t span = 0;  // long records: the sparse walk, one launch set for any size
+    if ((st = sparse_choice(c, input, start, len, e, true, stream, span))) return st;
+    probe_note(c, input, start, len, e, o->summary);
+    if (span) {
+      SpanScope scope{c};
+      c->sparse_span = span;
+      return launch_range(c, input, len, start, len, e, 0, start, nullptr, o, stream);
+    }
+    if (len - start > (uint64_t)c->res_waves * npr::kResSlots * npr::kTile)
+      return npr_dev_parse_extract_chunked(c, input, len, start, e, o, 0, stream);
+    return launch_range(c, input, len, start, len, e, 0, start, nullptr, o, stream);
+  }
+  return npr_dev_parse_extract_range(c, input, len, start, len, e, 0, start, o, stream);
+}
+
 // the epoch of the last launch that wrote summary s (0: none of ours)
 static uint32_t summary_epoch(const npr_ctx *c, const npr_summary *s) {
   for (auto it = c->sum_log.rbegin(); it != c->sum_log.rend(); ++it)
@@ -625,12 +638,14 @@ static npr_status range_params(npr_ctx *c, const void *input, uint64_t len, uint
 npr_status npr_dev_parse_extract_range(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness e, int speculative_start,
                                        uint64_t ref_record, const npr_dev_outputs *o, void *stream) {
+  if (c && o) probe_unbind(c, o->summary);
   return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream);
 }
 
 npr_status npr_dev_parse_extract_chain(npr_ctx *c, const void *input, uint64_t len, uint64_t start,
                                        uint64_t stop, npr_endianness e, const npr_summary *prev,
                                        uint64_t ref_record, const npr_dev_outputs *o, void *stream) {
+  if (c && o) probe_unbind(c, o->summary);
   return launch_range(c, input, len, start, stop, e, 0, ref_record, prev, o, stream);
 }
 
@@ -649,6 +664,7 @@ static npr_status chained(npr_ctx *c, const void *input, uint64_t len, uint64_t 
                           npr_endianness e, int speculative_start, uint64_t ref_record, const npr_dev_outputs *o,
                           uint64_t chunk_bytes, void *stream, const ShardSpec *sh) {
   const bool flows_only = !o->record_offsets && !o->records && !o->record_status;
+  probe_unbind(c, o->summary);  // (noted below when this parse chooses by the capture's density)
   if (!c->resident || !flows_only || stop <= start)
     return launch_range(c, input, len, start, stop, e, speculative_start, ref_record, nullptr, o, stream, sh);
   npr_status st = res_geometry(c);

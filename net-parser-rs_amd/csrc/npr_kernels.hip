@@ -630,7 +630,7 @@ __device__ __forceinline__ void stamp_flush(const ParseParams &kp, const Stamps 
 // 16-B read per lane); only the survivors, in offset order, have their chain graded.
 // (the capture's length by value, not the ParseParams: a by-reference kernel argument reaching a
 // call the compiler does not inline is copied to scratch memory first)
-__device__ uint64_t speculate(SpecCtx sc, uint64_t len, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
+__device__ __forceinline__ uint64_t speculate(SpecCtx sc, uint64_t len, const uint32_t *w, uint64_t tile_lo, uint32_t lo,
                               uint32_t span) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t avail = len - tile_lo;

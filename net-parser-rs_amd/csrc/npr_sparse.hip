@@ -600,6 +600,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
   __shared__ Seg E0, TOT;
   __shared__ uint32_t rows[kResolvers * kSpRow];
   __shared__ uint32_t task[kTasks], ntask, npass;  // the resolve's re-walk tasks: flagged index << 6 | lane
+                                                   // (slots 0..63: the lowest flagged group's, reserved)
   __shared__ uint64_t tpos[kTasks];                // ... and each task's exact entry
   const ParseParams &kp = sp.kp;
   const uint32_t tid = threadIdx.x, W = sp.ngroups;
@@ -836,7 +837,10 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
     // incoming state and its lanes' CURRENT exits, the position entering each lane; lanes a record
     // spans are set passed over, every lane whose entry differs becomes a re-walk task, and all 256
     // threads take the tasks.  Repeat until no lane changes: each pass makes at least the first
-    // inconsistent lane of every group exact, so it ends, and its fixed point is the serial rule's.
+    // inconsistent lane of the LOWEST flagged group exact (its tasks have 64 reserved queue slots;
+    // the other groups share the rest, and what does not fit waits for the next pass), so the lowest
+    // group settles within 65 passes, and the fixed point is the serial rule's.  Each scan round
+    // therefore settles its lowest flagged group for good (the outer `round` bound relies on that).
     // Round 4's one thread per group walked a group's lanes in turn: 15.3 ms of
     // the 300-MB adversarial capture's 16.3 (901 re-walks).
     const uint32_t nr = nbad < (uint32_t)kResolvers ? nbad : (uint32_t)kResolvers;
@@ -848,6 +852,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
           ntask = 0;
           npass = 0;
         }
+        if (tid < 64) task[tid] = ~0u;  // the lowest group's reserved slots: empty unless claimed
         __syncthreads();
         for (uint32_t b = wv; b < nr; b += kScanThreads / 64) {  // (a) the tasks of group bad[b]
           const uint32_t w = bad[b];
@@ -874,20 +879,22 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
                 atomicAdd(&npass, 1u);
               }
             } else if (L.entry != pred) {  // mis-speculated (or its predecessor moved): walk again
-              const uint32_t k = atomicAdd(&ntask, 1u);
+              const uint32_t k = b == 0 ? lane : 64u + atomicAdd(&ntask, 1u);
               if (k < kTasks) {
                 task[k] = (b << 6) | lane;
                 tpos[k] = pred;
               }
+              if (b == 0) atomicAdd(&npass, 1u);  // (a pass with only reserved tasks still runs)
             }
           }
         }
         fence_agent();
         __syncthreads();
         fence_agent();
-        const uint32_t nt = ntask < kTasks ? ntask : kTasks;
-        if (nt == 0 && npass == 0) break;
+        const uint32_t nt = ntask < kTasks - 64u ? 64u + ntask : kTasks;
+        if (ntask == 0 && npass == 0) break;
         for (uint32_t k = tid; k < nt; k += kScanThreads) {  // (b) every thread re-walks tasks
+          if (task[k] == ~0u) continue;  // an unclaimed reserved slot
           const uint32_t b = task[k] >> 6, j = task[k] & 63u, w = bad[b];
           const uint64_t li = (uint64_t)w * 64 + j, p = tpos[k];
           uint32_t cnt = 0;

@@ -5,6 +5,7 @@ anything else — there is no CPU path in the product.
 """
 import ctypes
 import os
+import warnings
 
 import numpy as np
 
@@ -250,6 +251,8 @@ _SIGNATURES = {
                                           ctypes.c_uint64, _vp, ctypes.c_uint64, _vp, ctypes.c_int]),
 }
 
+ABI_VERSION = 5  # include/npr.h NPR_ABI_VERSION: the layout these bindings assume
+
 _lib = None
 
 
@@ -264,14 +267,30 @@ def load_library(path=None):
             f"libnpr.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the parser has no CPU fallback)")
     lib = ctypes.CDLL(p)
+    # An A/B build of an older revision (NPR_LIB) may predate a symbol or the ABI: that is refused
+    # unless NPR_LIB_ALLOW_OLD=1 says the experiment expects it; the product library
+    # must match exactly.
+    allow_old = p != LIB_PATH and os.environ.get("NPR_LIB_ALLOW_OLD") == "1"
+    abi_fn = getattr(lib, "npr_abi_version", None)
+    abi = abi_fn() if abi_fn is not None else None
+    if abi != ABI_VERSION:
+        msg = f"{p}: ABI {abi}, this package binds ABI {ABI_VERSION}"
+        if not allow_old:
+            raise ImportError(msg + " (set NPR_LIB_ALLOW_OLD=1 to load an older A/B build anyway)")
+        warnings.warn(msg)
+    missing = []
     for name, (res, args) in _SIGNATURES.items():
         fn = getattr(lib, name, None)
-        if fn is None:  # an A/B build of an older revision (NPR_LIB) may predate a symbol
-            if p == LIB_PATH:
-                raise ImportError(f"{p} does not export {name}")
+        if fn is None:
+            missing.append(name)
             continue
         fn.restype = res
         fn.argtypes = args
+    if missing:
+        msg = f"{p} does not export {', '.join(missing)}"
+        if not allow_old:
+            raise ImportError(msg)
+        warnings.warn(msg)
     if path is None:
         _lib = lib
     return lib

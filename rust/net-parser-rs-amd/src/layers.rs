@@ -8,8 +8,12 @@
 //!
 //! `flow::layer2::FlowExtraction` for `Ethernet` (src/flow/layer2/ethernet.rs:39-133) runs the frame
 //! through the device decoder (one record, one call), which is what the reference's flow path
-//! composes from these objects; the layer-3 / layer-4 `FlowExtraction` traits (which take the outer
-//! layers' flow info) are not restated.
+//! composes from these objects.  The layer-3 / layer-4 `FlowExtraction` traits, which take the
+//! outer layers' flow info, are restated on the host exactly as the reference composes them:
+//! `IPv4` / `IPv6` parse their payload with `Tcp::parse` / `Udp::parse` (libnpr's host parsers),
+//! reject a remainder, and hand their info to the layer-4 object, which builds the `Flow`
+//! (src/flow/layer3/{ipv4,ipv6,arp}.rs, src/flow/layer4/{tcp,udp}.rs).  No device work: these are
+//! per-object calls on objects the caller already parsed.
 
 use std::net::{IpAddr, Ipv4Addr, Ipv6Addr};
 
@@ -306,6 +310,79 @@ pub enum Layer3<'a> {
     Arp(Arp),
     IPv4(IPv4<'a>),
     IPv6(IPv6<'a>),
+}
+
+// ---- the layer-3 flow dispatch: src/flow/layer3/{ipv4,ipv6,arp}.rs ---------------------------------
+use crate::flow::info::layer2::Info as L2Info;
+use crate::flow::info::layer3::{Id as L3Id, Info as L3Info};
+use crate::flow::info::layer4::{Id as L4Id, Info as L4Info};
+use crate::flow::layer3::errors::Error as L3Error;
+use crate::flow::layer4::FlowExtraction as Layer4Extraction;
+
+// IPv4 / IPv6 share the reference's dispatch (src/flow/layer3/ipv4.rs:49-101, ipv6.rs:49-100):
+// TCP and UDP parse their payload and must leave no remainder, any other protocol is an error.
+// `wrap` makes the IP version's layer-3 error (IPv4 / IPv6 variant) of an ip_errors-shaped error.
+macro_rules! ip_flow {
+    ($payload:expr, $protocol:expr, $l2:expr, $l3:expr, $errs:ident, $wrap:expr) => {{
+        let proto: InternetProtocolId = $protocol;
+        let wrap = $wrap;
+        let l4_err = |e: crate::flow::layer3::$errs::errors::Error| -> crate::flow::errors::Error {
+            let e: L3Error = wrap(e);
+            e.into()
+        };
+        match proto {
+            InternetProtocolId::Tcp => match Tcp::parse($payload) {
+                Err(err) => Err(l4_err(crate::flow::layer3::$errs::errors::Error::NetParser { l4: proto, err })),
+                Ok((rem, l4)) if rem.is_empty() => l4.extract_flow($l2, $l3),
+                Ok((rem, _)) => Err(l4_err(crate::flow::layer3::$errs::errors::Error::Incomplete { l4: proto, size: rem.len() })),
+            },
+            InternetProtocolId::Udp => match Udp::parse($payload) {
+                Err(err) => Err(l4_err(crate::flow::layer3::$errs::errors::Error::NetParser { l4: proto, err })),
+                Ok((rem, l4)) if rem.is_empty() => l4.extract_flow($l2, $l3),
+                Ok((rem, _)) => Err(l4_err(crate::flow::layer3::$errs::errors::Error::Incomplete { l4: proto, size: rem.len() })),
+            },
+            _ => Err(l4_err(crate::flow::layer3::$errs::errors::Error::InternetProtocolId { id: proto })),
+        }
+    }};
+}
+
+/// <IPv4 as FlowExtraction>::extract_flow (src/flow/layer3/ipv4.rs:40-103)
+impl<'a> crate::flow::layer3::FlowExtraction for IPv4<'a> {
+    fn extract_flow(&self, l2: L2Info) -> Result<crate::flow::Flow, crate::flow::errors::Error> {
+        let l3 = L3Info { id: L3Id::IPv4, src_ip: self.src_ip, dst_ip: self.dst_ip };
+        ip_flow!(self.payload, self.protocol, l2, l3, ipv4, L3Error::IPv4)
+    }
+}
+
+/// <IPv6 as FlowExtraction>::extract_flow (src/flow/layer3/ipv6.rs:40-102)
+impl<'a> crate::flow::layer3::FlowExtraction for IPv6<'a> {
+    fn extract_flow(&self, l2: L2Info) -> Result<crate::flow::Flow, crate::flow::errors::Error> {
+        let l3 = L3Info { id: L3Id::IPv6, src_ip: self.src_ip, dst_ip: self.dst_ip };
+        ip_flow!(self.payload, self.protocol, l2, l3, ipv6, L3Error::IPv6)
+    }
+}
+
+/// <Arp as FlowExtraction>::extract_flow (src/flow/layer3/arp.rs:23-27): never a flow
+impl crate::flow::layer3::FlowExtraction for Arp {
+    fn extract_flow(&self, _l2: L2Info) -> Result<crate::flow::Flow, crate::flow::errors::Error> {
+        let e: L3Error = crate::flow::layer3::arp::errors::Error::Flow.into();
+        Err(e.into())
+    }
+}
+
+// ---- the layer-4 flow: src/flow/layer4/{tcp,udp}.rs ------------------------------------------------
+/// <Tcp as FlowExtraction>::extract_flow (src/flow/layer4/tcp.rs:23-35)
+impl<'a> Layer4Extraction for Tcp<'a> {
+    fn extract_flow(&self, l2: L2Info, l3: L3Info) -> Result<crate::flow::Flow, crate::flow::errors::Error> {
+        Ok(crate::flow::Flow::new(l2, l3, L4Info { id: L4Id::Tcp, dst_port: self.dst_port, src_port: self.src_port }))
+    }
+}
+
+/// <Udp as FlowExtraction>::extract_flow (src/flow/layer4/udp.rs:23-35)
+impl<'a> Layer4Extraction for Udp<'a> {
+    fn extract_flow(&self, l2: L2Info, l3: L3Info) -> Result<crate::flow::Flow, crate::flow::errors::Error> {
+        Ok(crate::flow::Flow::new(l2, l3, L4Info { id: L4Id::Udp, dst_port: self.dst_port, src_port: self.src_port }))
+    }
 }
 
 // ---- layer 4: src/layer4/{tcp,udp,vxlan}.rs -------------------------------------------------------

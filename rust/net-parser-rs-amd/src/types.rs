@@ -515,6 +515,11 @@ pub mod flow_types {
 
     /// src/flow/layer3/{mod,arp,ipv4,ipv6}.rs
     pub mod layer3 {
+        /// src/flow/layer3/mod.rs:9-11 (implemented for layer3::{IPv4, IPv6, Arp} in crate::layers)
+        pub trait FlowExtraction {
+            fn extract_flow(&self, l2: super::info::layer2::Info) -> Result<crate::flow::Flow, crate::flow::errors::Error>;
+        }
+
         pub mod errors {
             wrap!(Error {
                 Arp(super::arp::errors::Error) => "ARP Error: " debug,
@@ -591,6 +596,15 @@ pub mod flow_types {
 
     /// src/flow/layer4/{mod,tcp,udp,vxlan}.rs
     pub mod layer4 {
+        /// src/flow/layer4/mod.rs:10-12 (implemented for layer4::{Tcp, Udp} in crate::layers)
+        pub trait FlowExtraction {
+            fn extract_flow(
+                &self,
+                l2: super::info::layer2::Info,
+                l3: super::info::layer3::Info,
+            ) -> Result<crate::flow::Flow, crate::flow::errors::Error>;
+        }
+
         pub mod errors {
             wrap!(Error {
                 Tcp(super::tcp::errors::Error) => "Tcp Error: " debug,

@@ -306,3 +306,62 @@ fn ethernet_flow_extraction_matches_reference() {
         }
     }
 }
+
+#[test]
+fn layer3_and_layer4_flow_extraction_match_reference() {
+    // <IPv4 | IPv6 | Arp as flow::layer3::FlowExtraction>::extract_flow(l2) over every Ethernet
+    // payload of the capture (and every prefix of a few), and <Tcp | Udp as
+    // flow::layer4::FlowExtraction>::extract_flow(l2, l3) on the parsed L4 objects: the same Flow or
+    // the same error (Debug), src/flow/layer3/{ipv4,ipv6,arp}.rs, src/flow/layer4/{tcp,udp}.rs
+    use amd::flow::layer3::FlowExtraction as _;
+    use amd::flow::layer4::FlowExtraction as _;
+    use net_parser_rs::flow::layer3::FlowExtraction as RefL3;
+    use net_parser_rs::flow::layer4::FlowExtraction as RefL4;
+    let data = capture();
+    let (_, fa) = net_parser_rs::CaptureFile::parse(&data).unwrap();
+    let recs = fa.records.into_inner();
+    let mut frames: Vec<&[u8]> = recs.iter().map(|r| r.payload).collect();
+    for f in recs.iter().take(40).map(|r| r.payload) {
+        for k in 0..f.len() {
+            frames.push(&f[..k]);
+        }
+    }
+    let mut compared = 0usize;
+    for (i, f) in frames.iter().enumerate() {
+        let (a, r) = match (amd::layer2::ethernet::Ethernet::parse(f), net_parser_rs::layer2::ethernet::Ethernet::parse(f)) {
+            (Ok((_, a)), Ok((_, r))) => (a, r),
+            _ => continue,
+        };
+        let al2 = amd::flow::info::layer2::Info {
+            id: amd::flow::info::layer2::Id::Ethernet,
+            src_mac: a.src_mac,
+            dst_mac: a.dst_mac,
+            vlan: a.vlan(),
+        };
+        let rl2 = net_parser_rs::flow::info::layer2::Info {
+            id: net_parser_rs::flow::info::layer2::Id::Ethernet,
+            src_mac: r.src_mac.clone(),
+            dst_mac: r.dst_mac.clone(),
+            vlan: r.vlan(),
+        };
+        if let (Ok((_, a4)), Ok((_, r4))) = (amd::layer3::ipv4::IPv4::parse(a.payload), net_parser_rs::layer3::ipv4::IPv4::parse(r.payload)) {
+            assert_eq!(format!("{:?}", a4.extract_flow(al2)), format!("{:?}", RefL3::extract_flow(&r4, rl2.clone())), "ipv4 flow {}", i);
+            let al3 = amd::flow::info::layer3::Info { id: amd::flow::info::layer3::Id::IPv4, src_ip: a4.src_ip, dst_ip: a4.dst_ip };
+            let rl3 = net_parser_rs::flow::info::layer3::Info { id: net_parser_rs::flow::info::layer3::Id::IPv4, src_ip: r4.src_ip, dst_ip: r4.dst_ip };
+            if let (Ok((_, at)), Ok((_, rt))) = (amd::layer4::tcp::Tcp::parse(a4.payload), net_parser_rs::layer4::tcp::Tcp::parse(r4.payload)) {
+                assert_eq!(format!("{:?}", at.extract_flow(al2, al3)), format!("{:?}", RefL4::extract_flow(&rt, rl2.clone(), rl3.clone())), "tcp flow {}", i);
+            }
+            if let (Ok((_, au)), Ok((_, ru))) = (amd::layer4::udp::Udp::parse(a4.payload), net_parser_rs::layer4::udp::Udp::parse(r4.payload)) {
+                assert_eq!(format!("{:?}", au.extract_flow(al2, al3)), format!("{:?}", RefL4::extract_flow(&ru, rl2.clone(), rl3.clone())), "udp flow {}", i);
+            }
+            compared += 1;
+        }
+        if let (Ok((_, a6)), Ok((_, r6))) = (amd::layer3::ipv6::IPv6::parse(a.payload), net_parser_rs::layer3::ipv6::IPv6::parse(r.payload)) {
+            assert_eq!(format!("{:?}", a6.extract_flow(al2)), format!("{:?}", RefL3::extract_flow(&r6, rl2.clone())), "ipv6 flow {}", i);
+        }
+        if let (Ok((_, aa)), Ok((_, ra))) = (amd::layer3::arp::Arp::parse(a.payload), net_parser_rs::layer3::arp::Arp::parse(r.payload)) {
+            assert_eq!(format!("{:?}", aa.extract_flow(al2)), format!("{:?}", RefL3::extract_flow(&ra, rl2.clone())), "arp flow {}", i);
+        }
+    }
+    assert!(compared > 1000, "{} IPv4 frames compared", compared);
+}

@@ -10,7 +10,8 @@ CRATE = "rust/net-parser-rs-amd"
 QUOTED = [("Cargo.toml", "toml"), ("build.rs", "rust"), ("src/ffi.rs", "rust")]
 LISTED = [("src/lib.rs", "the reference's record API (`src/lib.rs`, `record.rs`, `file.rs`, `global_header.rs`) over the C-ABI; `CaptureParser`"),
           ("src/types.rs", "the reference's public types, field for field (errors, header, ids, `Flow`, the flow error tree)"),
-          ("src/flow.rs", "`FlowExtraction`, `convert_records` and the batched/pipelined additions; device rows to `Flow` / errors")]
+          ("src/flow.rs", "`FlowExtraction`, `convert_records` and the batched/pipelined additions; device rows to `Flow` / errors"),
+          ("src/layers.rs", "the per-layer header objects (`Ethernet` ... `Vxlan`, `Layer2/3/4`) over the host layer parsers, and the layer-2/3/4 `FlowExtraction` impls")]
 MARK = "## 2. The crate, file by file"
 TAIL = "## 3. "
 

@@ -45,49 +45,113 @@ static int same_flows(const npr_flow *a, const npr_flow_v6 *a6, const npr_flow *
   return 1;
 }
 
-/* The flow of one frame composed from the per-layer host parsers, as the src/flow/layer2..4 modules
- * compose Ethernet -> IPv4 | IPv6 -> TCP | UDP (remainder checks included): 1 = a flow, 0 = an error. */
-static int layers_flow(const uint8_t *fr, size_t n, npr_flow *f, npr_flow_v6 *f6) {
+/* A Failure's input range, moved from the layer's input to the frame (npr_flow_details' encoding). */
+static uint64_t shift(uint64_t det, uint64_t off) {
+  return ((det & 0xFFFFFFFFull) + off) | (((det >> 32) + off) << 32);
+}
+
+/* The flow of one frame composed from the per-layer host parsers exactly as the reference's flow
+ * traits compose the layer objects, the chain the Rust crate's trait impls follow
+ * (rust/net-parser-rs-amd/src/layers.rs):
+ *   <Ethernet as layer2::FlowExtraction>      src/flow/layer2/ethernet.rs:39-133
+ *   <IPv4 | IPv6 | Arp as layer3::...>         src/flow/layer3/ipv4.rs:40-103, ipv6.rs:40-102, arp.rs:23-27
+ *   <Tcp | Udp as layer4::FlowExtraction>      src/flow/layer4/tcp.rs:23-35, udp.rs:23-35
+ * Returns the npr_flow_status leaf of the error the chain returns (NPR_FLOW_OK: *f, *f6 hold the
+ * flow) and *det the payload that error carries. */
+static int layers_flow(const uint8_t *fr, size_t n, npr_flow *f, npr_flow_v6 *f6, uint64_t *det_out) {
   npr_ethernet e;
   npr_vlan_tag tag[8];
   size_t used;
-  uint64_t det;
+  uint64_t det = 0;
   memset(f, 0, sizeof *f), memset(f6, 0, sizeof *f6);
+  *det_out = 0;
   const npr_status se = npr_ethernet_parse(fr, n, &e, tag, 8, &used, &det);
-  if (se != NPR_OK && se != NPR_ERR_CAPACITY) return 0;
-  const uint8_t *p = fr + e.payload_offset;
+  if (se == NPR_INCOMPLETE) return *det_out = det, NPR_FLOW_ETH_INCOMPLETE;  /* Error::NetParser */
+  if (se == NPR_FAILURE) return *det_out = det, NPR_FLOW_ETH_FAILURE;
+  const uint64_t off = e.payload_offset;
+  const uint8_t *p = fr + off;
   const uint64_t pn = e.payload_length;
   uint64_t l4off, l4len;
-  int proto;
-  if (e.ether_type == 0x0800) {
-    npr_ipv4 v;
-    if (npr_ipv4_parse(p, pn, &v, &used, &det) != NPR_OK || used != pn) return 0;
-    memcpy(f->src_ip, v.src_ip, 4), memcpy(f->dst_ip, v.dst_ip, 4);
-    l4off = v.payload_offset, l4len = v.payload_length, proto = v.protocol;
-  } else if (e.ether_type == 0x86DD) {
+  int proto, v6 = 0;
+  if (e.ether_type == 0x0800 || e.ether_type == 0x86DD) {
+    v6 = e.ether_type == 0x86DD;
+    npr_ipv4 v4;
     npr_ipv6 v;
-    if (npr_ipv6_parse(p, pn, &v, &used, &det) != NPR_OK || used != pn) return 0;
-    memcpy(f6->src_ip, v.src_ip, 16), memcpy(f6->dst_ip, v.dst_ip, 16);
-    f->kind |= NPR_FLOW_KIND_IPV6;
-    l4off = v.payload_offset, l4len = v.payload_length, proto = v.protocol;
+    const npr_status s3 = v6 ? npr_ipv6_parse(p, pn, &v, &used, &det) : npr_ipv4_parse(p, pn, &v4, &used, &det);
+    /* L2(Ethernet(NetParser{l3, err})) / L2(Ethernet(Incomplete{l3, size})) */
+    if (s3 == NPR_INCOMPLETE) return *det_out = det, v6 ? NPR_FLOW_L2_IPV6_INCOMPLETE : NPR_FLOW_L2_IPV4_INCOMPLETE;
+    if (s3 == NPR_FAILURE) return *det_out = shift(det, off), v6 ? NPR_FLOW_L2_IPV6_FAILURE : NPR_FLOW_L2_IPV4_FAILURE;
+    if (s3 == NPR_CUSTOM) return *det_out = det, v6 ? NPR_FLOW_L2_IPV6_CUSTOM : NPR_FLOW_L2_IPV4_CUSTOM;
+    if (used != pn) return *det_out = pn - used, v6 ? NPR_FLOW_L2_IPV6_REMAINDER : NPR_FLOW_L2_IPV4_REMAINDER;
+    if (v6) {
+      memcpy(f6->src_ip, v.src_ip, 16), memcpy(f6->dst_ip, v.dst_ip, 16);
+      f->kind |= NPR_FLOW_KIND_IPV6;
+      l4off = v.payload_offset, l4len = v.payload_length, proto = v.protocol;
+    } else {
+      memcpy(f->src_ip, v4.src_ip, 4), memcpy(f->dst_ip, v4.dst_ip, 4);
+      l4off = v4.payload_offset, l4len = v4.payload_length, proto = v4.protocol;
+    }
+  } else if (e.ether_type == 0x0806) {
+    npr_arp a;
+    if (npr_arp_parse(p, pn, &a, &used, &det) != NPR_OK) return *det_out = det, NPR_FLOW_L2_ARP_INCOMPLETE;
+    if (used != pn) return *det_out = pn - used, NPR_FLOW_L2_ARP_REMAINDER;
+    return NPR_FLOW_L3_ARP; /* L3(Arp(Flow)): ARP is never a flow */
   } else {
-    return 0;  /* ARP never yields a flow; LLDP / 802.3 lengths are L2 errors */
+    return *det_out = e.ether_type, NPR_FLOW_L2_ETHERTYPE; /* LLDP / an 802.3 length */
   }
+  /* L3(IPv4|IPv6(...)): the IP payload through Tcp::parse / Udp::parse, no remainder allowed */
+  const uint64_t fo = off + l4off; /* the L4 input's offset in the frame */
   if (proto == 6) {
     npr_tcp t;
-    if (npr_tcp_parse(p + l4off, l4len, &t, &used, &det) != NPR_OK) return 0;
-    f->src_port = t.src_port, f->dst_port = t.dst_port;
+    const npr_status s4 = npr_tcp_parse(p + l4off, l4len, &t, &used, &det);
+    if (s4 == NPR_INCOMPLETE) return *det_out = det, v6 ? NPR_FLOW_L3_IPV6_TCP_INCOMPLETE : NPR_FLOW_L3_IPV4_TCP_INCOMPLETE;
+    if (s4 != NPR_OK) return *det_out = shift(det, fo), v6 ? NPR_FLOW_L3_IPV6_TCP_FAILURE : NPR_FLOW_L3_IPV4_TCP_FAILURE;
+    f->src_port = t.src_port, f->dst_port = t.dst_port; /* payload = rest: never a remainder */
   } else if (proto == 17) {
     npr_udp u;
-    if (npr_udp_parse(p + l4off, l4len, &u, &used, &det) != NPR_OK || used != l4len) return 0;
+    if (npr_udp_parse(p + l4off, l4len, &u, &used, &det) != NPR_OK)
+      return *det_out = det, v6 ? NPR_FLOW_L3_IPV6_UDP_INCOMPLETE : NPR_FLOW_L3_IPV4_UDP_INCOMPLETE;
+    if (used != l4len) return *det_out = l4len - used, v6 ? NPR_FLOW_L3_IPV6_UDP_REMAINDER : NPR_FLOW_L3_IPV4_UDP_REMAINDER;
     f->src_port = u.src_port, f->dst_port = u.dst_port;
     f->kind |= NPR_FLOW_KIND_UDP;
   } else {
-    return 0;
+    return *det_out = (uint64_t)proto, v6 ? NPR_FLOW_L3_IPV6_PROTOCOL : NPR_FLOW_L3_IPV4_PROTOCOL;
   }
+  /* Flow::new (src/flow/mod.rs:64-86) from the layer-2 info */
   memcpy(f->src_mac, e.src_mac, 6), memcpy(f->dst_mac, e.dst_mac, 6);
   f->vlan = e.n_vlans ? tag[0].id : 0;
-  return 1;
+  return NPR_FLOW_OK;
+}
+
+/* The per-layer host parsers, composed as the layer-2/3/4 flow traits compose them, agree with the
+ * oracle's extract_flow on every record: the same error leaf and payload, or the same flow.  Host
+ * code only: it also runs without a device. */
+static void run_layers(const char *path, const uint8_t *in, const npr_record *orec, size_t on) {
+  /* the per-layer host parsers, composed as the layer-2/3/4 flow traits compose them, agree with the
+   * oracle's extract_flow on every record: the same error leaf and payload, or the same flow */
+  {
+    size_t agree = 0, errs = 0;
+    for (size_t i = 0; i < on; ++i) {
+      const uint8_t *fr = in + orec[i].offset + 16;
+      npr_flow lf, of;
+      npr_flow_v6 lf6, of6;
+      uint64_t ldet = 0, odet = 0;
+      const int lst = layers_flow(fr, orec[i].actual_length, &lf, &lf6, &ldet);
+      const int ost = or_extract_flow_detail(fr, orec[i].actual_length, 0, &of, &of6, &odet);
+      memset(of.record_offset, 0, 5), memset(lf.record_offset, 0, 5);
+      const int same = lst == ost && ldet == odet &&
+                       (ost != NPR_FLOW_OK || (!memcmp(&lf, &of, sizeof lf) &&
+                                               (!(of.kind & NPR_FLOW_KIND_IPV6) || !memcmp(&lf6, &of6, sizeof lf6))));
+      if (!same && agree + errs == i)
+        fprintf(stderr, "  first disagreement: record %zu status %d/%d detail %llu/%llu\n", i, lst, ost,
+                (unsigned long long)ldet, (unsigned long long)odet);
+      agree += same;
+      errs += !same;
+    }
+    CHECK(agree == on, "%s: layer traits agree with extract_flow (status, payload, flow) on %zu of %zu records", path,
+          agree, on);
+  }
+
 }
 
 static void run(npr_ctx *ctx, const char *path) {
@@ -107,22 +171,7 @@ static void run(npr_ctx *ctx, const char *path) {
   const int orc = or_capture_file_parse(in, len, &oh, orec, cap, &on, &ocons);
   const size_t onf = orc == OR_OK ? or_convert_records(in, len, orec, on, ofl, ofl6, cap) : 0;
 
-  /* the per-layer host parsers, composed, agree with the oracle's extract_flow on every record */
-  if (orc == OR_OK) {
-    size_t agree = 0;
-    for (size_t i = 0; i < on; ++i) {
-      const uint8_t *fr = in + orec[i].offset + 16;
-      npr_flow lf, of;
-      npr_flow_v6 lf6, of6;
-      const int ok = layers_flow(fr, orec[i].actual_length, &lf, &lf6);
-      const int ost = or_extract_flow(fr, orec[i].actual_length, 0, &of, &of6);
-      memset(of.record_offset, 0, 5), memset(lf.record_offset, 0, 5);
-      const int same = ok == (ost == 0) && (!ok || (!memcmp(&lf, &of, sizeof lf) &&
-                                                    (!(of.kind & NPR_FLOW_KIND_IPV6) || !memcmp(&lf6, &of6, sizeof lf6))));
-      agree += same;
-    }
-    CHECK(agree == on, "%s: layer parsers agree with extract_flow on %zu of %zu records", path, agree, on);
-  }
+  if (orc == OR_OK) run_layers(path, in, orec, on);
 
   /* GlobalHeader::parse (src/global_header.rs:40-70) */
   npr_global_header h;
@@ -298,8 +347,22 @@ int main(int argc, char **argv) {
   CHECK(npr_ctx_create(4096, &bad) == NPR_ERR_DEVICE && bad == NULL, "ctx_create(4096) must fail");
   CHECK(npr_ctx_create(0, NULL) == NPR_ERR_ARG, "ctx_create(NULL out)");
   if (npr_ctx_create(0, &ctx) != NPR_OK) {
-    fprintf(stderr, "no HIP device\n");
-    return 2;
+    /* no device: the host-only checks (the layer traits' composition) still run on the files */
+    for (int i = 1; i < argc; ++i) {
+      size_t len = 0;
+      uint8_t *in = slurp(argv[i], &len);
+      CHECK(in != NULL, "cannot read %s", argv[i]);
+      if (!in) continue;
+      const size_t cap = len / 16 + 2;
+      npr_record *orec = calloc(cap, sizeof *orec);
+      npr_global_header oh;
+      size_t on = 0, ocons = 0;
+      if (or_capture_file_parse(in, len, &oh, orec, cap, &on, &ocons) == OR_OK) run_layers(argv[i], in, orec, on);
+      free(orec);
+      free(in);
+    }
+    fprintf(stderr, "no HIP device (host-only checks: %d failures)\n", failures);
+    return failures ? 1 : 2;
   }
   for (int i = 1; i < argc; ++i) run(ctx, argv[i]);
   npr_ctx_destroy(ctx);

@@ -38,6 +38,20 @@ def test_library_is_gfx950_code_object():
     assert b"amdgcn-amd-amdhsa--gfx950" in data  # the offload bundle target id
 
 
+def test_no_kernel_has_a_private_segment():
+    """two fault-like events came from kernels that had gained a scratch segment
+    (round 4's k_flow_detail, round 5's res_bal variant).  Every kernel of the product's code object
+    keeps all its state in registers and LDS: the metadata note's .private_segment_fixed_size is 0
+    for each (msgpack positive fixint 0 right after the key), and no kernel has a dynamic stack."""
+    data = open(_abi.LIB_PATH, "rb").read()
+    key = b".private_segment_fixed_size"
+    vals = [data[m.end()] for m in re.finditer(re.escape(key), data)]
+    assert len(vals) >= 20, len(vals)  # every kernel of every translation unit
+    assert all(v == 0 for v in vals), vals
+    dyn = [data[m.end()] for m in re.finditer(re.escape(b".uses_dynamic_stack"), data)]
+    assert all(v == 0xc2 for v in dyn), dyn  # msgpack false
+
+
 def test_struct_sizes_match_c():
     import ctypes
     code = r'''
@@ -61,8 +75,24 @@ int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(npr_global
 
 def test_abi_version():
     lib = _abi.load_library()
-    assert lib.npr_abi_version() == 5
+    assert lib.npr_abi_version() == 5 == _abi.ABI_VERSION
     assert b"gfx950" in lib.npr_version()
+
+
+def test_loader_refuses_a_library_of_another_abi(tmp_path, monkeypatch):
+    """an A/B build (NPR_LIB) of another ABI is refused, not half-bound; NPR_LIB_ALLOW_OLD=1
+    loads it with a warning."""
+    src = tmp_path / "old.c"
+    src.write_text("int npr_abi_version(void) { return 4; }\n")
+    so = tmp_path / "libnpr_old.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", str(src), "-o", str(so)], check=True)
+    monkeypatch.delenv("NPR_LIB_ALLOW_OLD", raising=False)
+    with pytest.raises(ImportError, match="ABI 4"):
+        _abi.load_library(str(so))
+    monkeypatch.setenv("NPR_LIB_ALLOW_OLD", "1")
+    with pytest.warns(UserWarning):
+        lib = _abi.load_library(str(so))
+    assert lib.npr_abi_version() == 4
 
 
 @pytest.mark.parametrize("name", ["global_header_native_endian", "global_header_not_native_endian"])

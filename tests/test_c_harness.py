@@ -27,6 +27,26 @@ def test_harness_builds_and_refuses_without_gpu():
     assert r.returncode == 2 and "no HIP device" in r.stderr
 
 
+def test_harness_layer_traits_on_the_host(tmp_path):
+    """The layer-2/3/4 FlowExtraction chain composed from libnpr's host layer parsers (what the Rust
+    crate's trait impls do, rust/net-parser-rs-amd/src/layers.rs) gives the oracle's status leaf,
+    error payload and flow on every record (the harness's host-only checks; no device needed)."""
+    import torch
+    exe = build()
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: the gpu test runs the same checks")
+    paths = []
+    for name, blob in {"quirk": synth.quirk_corpus(5_000, seed=91), "quirk_be": synth.quirk_corpus(3_000, seed=92, big=True),
+                       "adversarial": synth.quirk_corpus(2_000, seed=93, fake_every=3, zero_every=7, jumbo_every=150,
+                                                         tail="truncated_payload"),
+                       "flow_mix": synth.flow_mix(3_000)}.items():
+        p = tmp_path / f"{name}.pcap"
+        p.write_bytes(blob)
+        paths.append(str(p))
+    r = subprocess.run([exe] + paths, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "host-only checks: 0 failures" in r.stderr, r.stdout + r.stderr
+
+
 @pytest.mark.gpu
 def test_harness_on_device(tmp_path):
     exe = build()

@@ -67,3 +67,28 @@ def test_host_entry_point_restages(captures):
     _, _, nf, cons, _ = device.host_parse_extract(b, with_v6=False, ctx=ctx)
     assert ctx.lib.npr_ctx_last_pass(ctx.handle) == _abi.PASS_RESIDENT
     assert nf == n_short and cons == 24 + 80 * n_short
+
+
+def test_one_workspace_alternating_buffers(captures):
+    """One Workspace (one summary buffer) alternating between a long-record capture and an 80-B one
+    at two addresses: checking one capture's parse must not rewrite the other's remembered density
+    (every entry that had held the summary pointer took the last parse's density)."""
+    long_, n_long, short, n_short = captures
+    L = len(long_)
+    a = torch.frombuffer(bytearray(long_), dtype=torch.uint8).cuda()
+    b = torch.frombuffer(bytearray(short), dtype=torch.uint8).cuda()
+    ws = device.Workspace(1, (L - 24) // 16 + 1, records=False, status=False, flows_v6=False)
+    for _ in range(3):
+        ws.launch(a)
+        sm = ws.check()
+        assert last_pass(ws) == _abi.PASS_SPARSE and sm.n_records == n_long
+        ws.launch(b)
+        sm = ws.check()
+        assert last_pass(ws) == _abi.PASS_RESIDENT and sm.n_records == n_short
+    # a caller's own range launch on the same summary corrects no entry either
+    ws.launch_range(b, 24, L)
+    sm = ws.check()
+    assert sm.n_records == n_short
+    ws.launch(a)
+    sm = ws.check()
+    assert last_pass(ws) == _abi.PASS_SPARSE and sm.n_records == n_long

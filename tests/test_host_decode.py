@@ -4,14 +4,15 @@ for the host and checked against the oracle on the CPU: status, flow fields and 
 import os
 import subprocess
 
+import pytest
+
 from net_parser_rs import synth
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DIR = os.path.join(REPO, "tests", "host_decode")
 
 
-def test_device_decoder_on_the_host_matches_oracle(tmp_path):
-    subprocess.run(["make", "-s", "-C", DIR], check=True)
+def corpora(tmp_path):
     caps = {
         "quirk.pcap": synth.quirk_corpus(4_000, seed=91),
         "quirk_be.pcap": synth.quirk_corpus(2_000, seed=92, big=True),
@@ -25,6 +26,14 @@ def test_device_decoder_on_the_host_matches_oracle(tmp_path):
         p = tmp_path / name
         p.write_bytes(blob)
         paths.append(str(p))
-    r = subprocess.run([os.path.join(DIR, "build", "decode_check")] + paths, capture_output=True, text=True,
-                       timeout=300)
+    return paths
+
+
+@pytest.mark.parametrize("exe", ["decode_check", "decode_check_san"])
+def test_device_decoder_on_the_host_matches_oracle(tmp_path, exe):
+    """decode_check_san: the same run under ASan + UBSan (any report aborts it: -fno-sanitize-recover),
+    VERDICT r05 item 2's sanitizer pass over the quirk corpora."""
+    subprocess.run(["make", "-s", "-C", DIR], check=True)
+    r = subprocess.run([os.path.join(DIR, "build", exe)] + corpora(tmp_path), capture_output=True, text=True,
+                       timeout=600, env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
     assert r.returncode == 0 and " 0 mismatches" in r.stdout, r.stdout + r.stderr

@@ -18,7 +18,7 @@ def test_integration_md_quotes_the_committed_crate():
     for f, body in blocks:
         assert body == open(os.path.join(CRATE, f)).read(), f"INTEGRATION.md is stale for {f}: run scripts/gen_integration.py"
     listed = re.findall(r"\| `rust/net-parser-rs-amd/([^`]+)` \| (\d+) \| `([0-9a-f]{16})` \|", doc)
-    assert {f for f, _, _ in listed} == {"src/lib.rs", "src/types.rs", "src/flow.rs"}
+    assert {f for f, _, _ in listed} == {"src/lib.rs", "src/types.rs", "src/flow.rs", "src/layers.rs"}
     for f, _, h in listed:
         got = hashlib.sha256(open(os.path.join(CRATE, f), "rb").read()).hexdigest()[:16]
         assert got == h, f"INTEGRATION.md is stale for {f}: run scripts/gen_integration.py"
