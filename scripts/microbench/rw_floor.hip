@@ -23,6 +23,14 @@
 //        load and a clock read per nap
 //   B    A without the per-wave A stores
 //   C    A with the nap reduced to s_sleep(2) and the abort word read every 16th nap only
+//   D    B, re-polling the missing granules with sc1 loads (no atomics), s_sleep(4), the abort
+//        word every 16th poll
+//   E    D with each workgroup's 5 granules stored and read as 16 + 16 + 8 B (dwordx4 sc1)
+//   F    E with the per-wave A stores issued after the look-back (behind the second barrier)
+//   N    E without the arrival counter
+//   Q    P with 5 granules per workgroup (5 sc1 stores; each poll reads all 5 by returning atomics)
+//   T    B with ONE granule per workgroup (the product's polling: sc1 once, then returning-atomic
+//        re-reads of the missing lanes, s_sleep(8) naps, an abort-word load per nap)
 //   G    grid-stride tile order (wave w: tiles w, w + W, ...), rows after each tile: the memory
 //        pattern of a pipelined pass that works through the capture in time order
 // The row width W is a run-time argument (32 = the npr_flow row; 16 and 8 = compact encodings;
@@ -116,6 +124,34 @@ __device__ __forceinline__ uint64_t ld_sc1(const uint64_t *p) {
 __device__ __forceinline__ void st_sc1(uint64_t *p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// two granules in one 16-B write-through (sc1) store (R2: observed untorn on gfx950 for 16-B sc1 halves)
+__device__ __forceinline__ void st16(uint64_t *p, uint64_t x, uint64_t y) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, 16, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(u32x4{(uint32_t)x, (uint32_t)(x >> 32), (uint32_t)y, (uint32_t)(y >> 32)}, rs, 0,
+                                         0, 16);
+}
+__device__ __forceinline__ bool tg(uint64_t w, uint32_t tag);
+// a workgroup's 5 granules: 8-B sc1 loads or returning atomics, or (WIDE) 16 + 16 + 8-B sc1 loads
+template <bool WIDE, bool ATOMIC, int NG = 5>
+__device__ __forceinline__ bool load5(uint64_t *g, uint32_t tag) {
+  if (NG == 1) return tg(ATOMIC ? __hip_atomic_fetch_add(g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), tag);
+  uint64_t x[5];
+  if (ATOMIC) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) x[k] = __hip_atomic_fetch_add(g + k, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (WIDE) {
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)g, 0, 40, 0x00020000);
+    const u32x4 v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, 0, 0, 16), v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, 16, 0, 16);
+    x[0] = ((uint64_t)v0[1] << 32) | v0[0], x[1] = ((uint64_t)v0[3] << 32) | v0[2];
+    x[2] = ((uint64_t)v1[1] << 32) | v1[0], x[3] = ((uint64_t)v1[3] << 32) | v1[2];
+    x[4] = __hip_atomic_load(g + 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) x[k] = __hip_atomic_load(g + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return tg(x[0], tag) && tg(x[1], tag) && tg(x[2], tag) && tg(x[3], tag) && tg(x[4], tag);
+}
 __device__ __forceinline__ uint64_t gr(uint32_t tag, uint64_t v) { return ((uint64_t)tag << 48) | (v & ((1ull << 48) - 1)); }
 __device__ __forceinline__ bool tg(uint64_t w, uint32_t tag) { return (uint32_t)(w >> 48) == (tag & 0xffffu); }
 
@@ -179,6 +215,11 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
   if (threadIdx.x == 0) fail = 0;
   __syncthreads();
   const uint32_t b = blockIdx.x, tag = a.target & 0xffffu;
+  constexpr bool kLook = MODE == 'A' || MODE == 'B' || MODE == 'C' || MODE == 'D' || MODE == 'E' || MODE == 'F' ||
+                        MODE == 'N' || MODE == 'T';
+  constexpr int kNg = MODE == 'T' ? 1 : 5;  // granules per workgroup aggregate
+  constexpr bool kSc1Poll = MODE == 'D' || MODE == 'E' || MODE == 'F' || MODE == 'N';
+  constexpr bool kWide = MODE == 'E' || MODE == 'F' || MODE == 'N';
   if (MODE == 'A' || MODE == 'C') {  // every wave's A after the barrier (the product's order)
     if (lane == 0) {
       uint64_t *p = a.agr + (uint64_t)v * kLine64;
@@ -216,15 +257,29 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
         }
         __builtin_amdgcn_s_sleep(4);
       }
-    } else if (MODE == 'P' || MODE == 'S') {  // one 8-B granule per workgroup, one line each
-      if (lane == 0) st_sc1(a.gran + (uint64_t)b * kLine64, gr(tag, b));
+    } else if (MODE == 'P' || MODE == 'S' || MODE == 'Q') {  // one (Q: five) 8-B granule(s) per workgroup, one line each
+      if (lane == 0) {
+        st_sc1(a.gran + (uint64_t)b * kLine64, gr(tag, b));
+        if (MODE == 'Q')
+#pragma unroll
+          for (int k = 1; k < 5; ++k) st_sc1(a.gran + (uint64_t)b * kLine64 + k, gr(tag, b + k));
+      }
       for (;;) {
         bool miss = false;
         for (uint32_t w0 = 0; w0 < b; w0 += 64) {
           const uint32_t i = w0 + lane;
           uint64_t *p = a.gran + (uint64_t)i * kLine64;
-          const uint64_t f = i < b ? (MODE == 'P' ? ld_atomic(p) : ld_sc1(p)) : gr(tag, 0);
-          miss = miss || __ballot(!tg(f, tag)) != 0ull;
+          bool got = true;
+          if (i < b) {
+            if (MODE == 'Q') {
+              const uint64_t x0 = ld_atomic(p), x1 = ld_atomic(p + 1), x2 = ld_atomic(p + 2), x3 = ld_atomic(p + 3),
+                             x4 = ld_atomic(p + 4);
+              got = tg(x0, tag) && tg(x1, tag) && tg(x2, tag) && tg(x3, tag) && tg(x4, tag);
+            } else {
+              got = tg(MODE == 'P' ? ld_atomic(p) : ld_sc1(p), tag);
+            }
+          }
+          miss = miss || __ballot(!got) != 0ull;
         }
         if (!miss) break;
         if (timed_out(a, t0)) {
@@ -233,12 +288,18 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
         }
         __builtin_amdgcn_s_sleep(4);
       }
-    } else {  // A / B / C: the resident pass's G publication and look-back
+    } else if (kLook) {  // A ... N: the resident pass's G publication and look-back
       if (lane == 0) {
         uint64_t *g = a.gran + (uint64_t)b * kLine64;
+        if (kWide) {
+          st16(g, gr(tag, b), gr(tag, b + 1));
+          st16(g + 2, gr(tag, b + 2), gr(tag, b + 3));
+          st_sc1(g + 4, gr(tag, b + 4));
+        } else {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) st_sc1(g + k, gr(tag, b + k));
-        (void)__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          for (int k = 0; k < kNg; ++k) st_sc1(g + k, gr(tag, b + k));
+        }
+        if (MODE != 'N') (void)__hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       constexpr int kWin = 4;
       bool have[kWin];
@@ -246,11 +307,7 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
       for (int w = 0; w < kWin; ++w) {  // every window once, sc1
         const uint32_t i = 64u * w + lane;
         have[w] = true;
-        if (i < b) {
-          const uint64_t *g = a.gran + (uint64_t)i * kLine64;
-          const uint64_t x0 = ld_sc1(g), x1 = ld_sc1(g + 1), x2 = ld_sc1(g + 2), x3 = ld_sc1(g + 3), x4 = ld_sc1(g + 4);
-          have[w] = tg(x0, tag) && tg(x1, tag) && tg(x2, tag) && tg(x3, tag) && tg(x4, tag);
-        }
+        if (i < b) have[w] = load5<kWide, false, kNg>(a.gran + (uint64_t)i * kLine64, tag);
       }
       uint32_t nap = 1;
       for (int tries = 0;; ++tries) {
@@ -259,7 +316,13 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
         for (int w = 0; w < kWin; ++w) miss = miss || __ballot(!have[w]) != 0ull;
         if (!miss) break;
         if (tries) {
-          if (MODE == 'C') {
+          if (kSc1Poll) {
+            __builtin_amdgcn_s_sleep(4);
+            if ((tries & 15) == 0 && timed_out(a, t0)) {
+              fail = 1;
+              break;
+            }
+          } else if (MODE == 'C') {
             __builtin_amdgcn_s_sleep(2);
             if ((tries & 15) == 0 && timed_out(a, t0)) {
               fail = 1;
@@ -278,12 +341,7 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
         for (int w = 0; w < kWin; ++w) {
           const uint32_t i = 64u * w + lane;
           if (__ballot(!have[w])) {
-            if (!have[w]) {
-              uint64_t *g = a.gran + (uint64_t)i * kLine64;
-              const uint64_t x0 = ld_atomic(g), x1 = ld_atomic(g + 1), x2 = ld_atomic(g + 2), x3 = ld_atomic(g + 3),
-                             x4 = ld_atomic(g + 4);
-              have[w] = tg(x0, tag) && tg(x1, tag) && tg(x2, tag) && tg(x3, tag) && tg(x4, tag);
-            }
+            if (!have[w]) have[w] = load5<kWide, !kSc1Poll, kNg>(a.gran + (uint64_t)i * kLine64, tag);
           }
         }
       }
@@ -291,6 +349,11 @@ __global__ __launch_bounds__(kWg * 64) void k_rw(Args a) {
   }
   __syncthreads();
   if (fail) return;
+  if (MODE == 'F' && lane == 0) {  // the per-wave A stores, deferred past the look-back
+    uint64_t *p = a.agr + (uint64_t)v * kLine64;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) st_sc1(p + k, gr(tag, c0 + k));
+  }
   for (uint32_t t = c0; t < c1; ++t) put_block(a, t, acc);
 }
 
@@ -399,6 +462,15 @@ int main(int argc, char **argv) {
       RUN('A', 32, "A resident pass's publication + look-back", rb);
       RUN('B', 32, "B = A without the per-wave A stores", rb);
       RUN('C', 32, "C = A with short naps, abort word every 16th", rb);
+      RUN('D', 32, "D = B with sc1 re-polls, s_sleep(4)", rb);
+      RUN('E', 32, "E = D with 16-B granule pairs", rb);
+      RUN('F', 32, "F = E with the A stores after the look-back", rb);
+      RUN('N', 32, "N = E without the arrival counter", rb);
+      RUN('Q', 32, "Q = P with 5 granules per workgroup", rb);
+      RUN('T', 32, "T = B with one granule per workgroup", rb);
+      for (uint32_t wb : {16u, 8u, 0u}) {
+        RUN('P', wb, "P 8-B granule per line, atomic polls", rb);
+      }
     }
   }
 #undef RUN
