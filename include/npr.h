@@ -262,7 +262,7 @@ npr_status npr_ctx_read_stamps(npr_ctx *ctx, uint64_t *out, uint64_t cap, uint64
  *   one 112-B window per record instead of streaming every payload byte.  0 chooses it from the
  *   record density of the capture's first 256 KiB (at least 256 MiB past `start`, a known start, no
  *   shard); 1 never; 2 always (lane ranges sized from the density, else 16 KiB); N >= 64 always,
- *   with lane ranges of N bytes (a test knob).  Same results either way.
+ *   with lane ranges of min(N, 256 KiB) bytes (a test knob).  Same results either way.
  * NPR_OPT_SPARSE_CAP (default 0 = 96): record slots per sparse lane; a lane with more records
  *   walks the rest again when its rows are written (a test knob; 1 .. 128).
  */

@@ -270,7 +270,7 @@ npr_status sparse_choice(npr_ctx *c, const void *input, uint64_t start, uint64_t
     const npr_status st = probe_density(c, input, start, stop, e, stream, mean, n);
     if (st) return st;
   }
-  uint64_t sized = std::min<uint64_t>(std::max<uint64_t>(kSparseSpanRecords * mean, 4u << 10), 1u << 20);
+  uint64_t sized = std::min<uint64_t>(std::max<uint64_t>(kSparseSpanRecords * mean, 4u << 10), npr::kSparseSpanMax);
   // A range of more records than one 256-lane workgroup per CU holds at ~24 each: k workgroups per CU
   // exactly (k = the fewest that keep lanes at <= 64 mean records: fewer lanes speculate less).  The walk is bound per CU (its
   // random 16-B loads), so its time follows the most lane-records any CU holds: C3 at 36.9 … 61 KB
@@ -283,7 +283,7 @@ npr_status sparse_choice(npr_ctx *c, const void *input, uint64_t start, uint64_t
       const uint64_t range = stop - start, est = range / mean, slots = (uint64_t)cus * kSparseCuLanes;
       if (est >= 24 * slots) {
         const uint64_t k = (est + slots * kSparseLaneRecords - 1) / (slots * kSparseLaneRecords);
-        sized = std::min<uint64_t>(std::max<uint64_t>((range + k * slots - 1) / (k * slots), 4u << 10), 1u << 20);
+        sized = std::min<uint64_t>(std::max<uint64_t>((range + k * slots - 1) / (k * slots), 4u << 10), npr::kSparseSpanMax);
       }
     }
   }
@@ -771,7 +771,7 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
                                 hipStream_t s, uint64_t span) {
   npr::SparseParams sp{};
   const uint64_t range = p.stop > p.start ? p.stop - p.start : 0;
-  sp.span = span;
+  sp.span = std::min<uint64_t>(span, npr::kSparseSpanMax);  // (a slot keeps 18 bits of record offset)
   sp.nlanes = (range + span - 1) / span;
   const uint64_t ng = (sp.nlanes + 63) / 64;
   if (ng > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large for the sparse walk");
@@ -782,7 +782,8 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
                  o_lite = o_first + a256(ng * 8), o_pre = o_lite + a256(3 * ng * 8),
                  o_scan = o_pre + a256(ng * sizeof(npr::SparsePre)),
                  o_ctl = o_scan + a256(npr::sparse_scan_words(ng) * 8), o_area = o_ctl + 256,
-                 total = o_area + (o->flows ? ng * sp.cap * 64 * 32 : 0);
+                 o_area_b = o_area + a256(ng * sp.cap * 64 * 16),
+                 total = o->flows ? o_area_b + ng * sp.cap * 64 * 12 : o_area;
   npr_status st = ensure(c, c->sparse, total);
   if (st) return st;
   char *b = (char *)c->sparse.p;
@@ -794,6 +795,7 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
   sp.lite = (uint64_t *)(b + o_lite);
   sp.ctl = (uint64_t *)(b + o_ctl);
   sp.area = o->flows ? (uint32_t *)(b + o_area) : nullptr;
+  sp.area_b = o->flows ? (uint32_t *)(b + o_area_b) : nullptr;
   if ((st = next_epoch(c, s))) return st;
   p.epoch = c->epoch;
   p.timeout_ticks = kTimeoutTicks;

@@ -179,8 +179,10 @@ struct SparseParams {
   uint64_t *first_entry;  // [ngroups]: the group's first lane entry found (speculative starts)
   SparsePre *pre;         // [ngroups]
   uint64_t *ctl;          // [0] = {epoch, 1} once the scan finished exact (the row kernel checks it)
-  uint32_t *area;         // slots: 32-B row (group cap + k) 64 + lane = record k of the lane
-                          // (row image; IPv6: word 0 = the address block's payload offset)
+  uint32_t *area;         // slots, record k of lane l of group g at slot r = (g cap + k) 64 + l, in two
+                          // arrays (28 B per record): area[16 B x r] = {ip_s (IPv6: the address
+  uint32_t *area_b;       // block's payload offset), ip_d, ports, smac01 | dmac45 << 16} and
+                          // area_b[12 B x r] = {smac2..5, dmac0..3, vlan:12 | kind:2 | offset - lane start:18}
   uint64_t *scan;         // k_sparse_scan's scratch: sparse_scan_words(ngroups) words
   uint64_t *lite;         // the aggregates' link fields as arrays: entry [ngroups], exit [ngroups],
                           // cnt | ok << 32 | valid << 63 [ngroups] (the scan's fast path loads these)
@@ -188,6 +190,8 @@ struct SparseParams {
 constexpr uint64_t sparse_scan_words(uint64_t ngroups) { return 7 * ngroups + 2; }
 hipError_t launch_sparse(const SparseParams &sp, hipStream_t s);
 constexpr uint32_t kSparseCapDefault = 96;  // slots per lane (<= kSparseCapMax: two mask words)
+constexpr uint32_t kSparseRelBits = 18;      // a slot's record offset, relative to its lane's start
+constexpr uint64_t kSparseSpanMax = 1ull << kSparseRelBits;  // lane ranges are at most this long
 constexpr uint32_t kSparseCapMax = 128;
 
 }  // namespace npr

@@ -1722,13 +1722,10 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   }
   if (wid == 0) {
     // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
-    // flows wait there, so the windows get the registers.
+    // flows wait there (stashed right after the publication, which does not wait for it), so the
+    // windows get the registers.  16-B chunks, lane-contiguous: ds_write_b128 / ds_read_b128.
     static_assert(kResSlots * 8 * 64 * 4 <= 2 * sizeof(ResShared), "stash fits two rings");
-    uint32_t *stash = &sh.w[0].data[0][0];
-#pragma unroll
-    for (int q = 0; q < kResSlots; ++q)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) stash[(q * 8 + j) * 64 + lane] = fl[q][j];
+    u32x4 *stash = reinterpret_cast<u32x4 *>(&sh.w[0].data[0][0]);
     // (1) the workgroup's waves, one per lane, from LDS: prefixes inside the workgroup + G(b)
     LaneSeg L{};
     if ((uint32_t)lane < nw) {
@@ -1752,6 +1749,11 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
     if (lane == 0) put_agg(kp, kp.rgroups + b, agg);
     if (lane == 0) (void)res_arrive(kp.rcnt);
     if (DIAG) stamp_at(st, 3);
+#pragma unroll
+    for (int q = 0; q < kResSlots; ++q) {
+      stash[(2 * q) * 64 + lane] = u32x4{fl[q][0], fl[q][1], fl[q][2], fl[q][3]};
+      stash[(2 * q + 1) * 64 + lane] = u32x4{fl[q][4], fl[q][5], fl[q][6], fl[q][7]};
+    }
     // (2) E(b) = anchor ⊕ G(0) ⊕ ... ⊕ G(b-1), looking back: every window read at once, then
     //     only the aggregates that are not this launch's yet re-read, until all are (a workgroup
     //     proceeds as soon as the ones below it are published, not when the whole grid is)
@@ -1817,9 +1819,14 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
     }
     wave_sync();
 #pragma unroll
-    for (int q = 0; q < kResSlots; ++q)
+    for (int q = 0; q < kResSlots; ++q) {
+      const u32x4 x = stash[(2 * q) * 64 + lane], y = stash[(2 * q + 1) * 64 + lane];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) fl[q][j] = stash[(q * 8 + j) * 64 + lane];
+      for (int j = 0; j < 4; ++j) {
+        fl[q][j] = x[j];
+        fl[q][4 + j] = y[j];
+      }
+    }
   }
   __syncthreads();
   if (sh.fail) return false;

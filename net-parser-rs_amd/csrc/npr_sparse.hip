@@ -358,26 +358,49 @@ __device__ __forceinline__ void row_image(const FlowWords &f, uint64_t p, u32x4 
   r1 = u32x4{f.d[4], f.d[5], f.d[6] | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
 }
 // every record of the lane into its slot (record k: slot k, while k < cap), Ok or not, so that a
-// wave's store instructions write 64 consecutive 32-B rows whatever its lanes decoded (Ok flows
-// only, densely, measured slower: lanes' slot indices drift apart at the first failed record, and
-// C3's walk went 479 -> 505 us); two mask words of the Ok ones, 96 slots (64: C3's 61-record lanes
-// overflowed into re-walks, rows 125 -> 111 us, walk 479 -> 489 us)
+// wave's store instructions write 64 consecutive slots whatever its lanes decoded (Ok flows only,
+// densely, measured slower: lanes' slot indices drift apart at the first failed record, and C3's
+// walk went 479 -> 505 us); two mask words of the Ok ones, 96 slots (64: C3's 61-record lanes
+// overflowed into re-walks, rows 125 -> 111 us, walk 479 -> 489 us).
+// A slot is 28 B in two arrays (npr_internal.hpp SparseParams::area / area_b): the 32-B row image
+// less what the rows kernel rebuilds -- the record offset from the lane's start (18 bits; lane
+// ranges are at most 256 KiB) and the flow kind's spare bits -- so each record's slot is one 16-B
+// and one 12-B store, and a wave's pair of store instructions writes 1 KiB + 768 B contiguously.
 // Slots and rows are plain (write-back) stores: non-temporal and write-through (sc1, sc0 sc1)
 // stores measured slower for both the scattered slot rows and the whole-line row blocks (DESIGN.md
 // §3.8)
-__device__ __forceinline__ void slot_store(u32x4 *d, u32x4 v) { *d = v; }
 __device__ __forceinline__ void row_store(u32x4 *d, u32x4 v) { *d = v; }
+// the 28-B slot image of a record at offset p of a lane starting at lo (p - lo < 2^18)
+__device__ __forceinline__ void slot_image(const FlowWords &f, uint64_t p, uint64_t lo, u32x4 &a, uint32_t (&b)[3]) {
+  const uint32_t m = 0u - ((f.d[6] >> 16) & NPR_FLOW_KIND_IPV6);  // (a mask: see row_image)
+  a = u32x4{(f.v6off & m) | (f.d[0] & ~m), f.d[1], f.d[2], (f.d[3] >> 16) | (f.d[6] << 16)};
+  b[0] = f.d[4];
+  b[1] = f.d[5];
+  b[2] = (f.d[3] & 0xfffu) | (((f.d[6] >> 16) & 3u) << 12) | ((uint32_t)(p - lo) << 14);
+}
+// the 32-B row of a slot (row_image's words) at file offset p
+__device__ __forceinline__ void slot_row(u32x4 a, uint32_t b0, uint32_t b1, uint32_t b2, uint64_t p, u32x4 &r0,
+                                         u32x4 &r1) {
+  r0 = u32x4{a[0], a[1], a[2], (b2 & 0xfffu) | (a[3] << 16)};
+  r1 = u32x4{b0, b1, (a[3] >> 16) | (((b2 >> 12) & 3u) << 16) | ((uint32_t)(p & 0xffu) << 24), (uint32_t)(p >> 8)};
+}
 struct AreaSink {
-  u32x4 *slot0;  // the lane's slot 0 (its first 16 B); NULL: count only
+  u32x4 *slot_a;     // the lane's slot 0 in area (16-B units); NULL: count only
+  uint32_t *slot_b;  // ... in area_b (dwords)
+  uint64_t lo;       // the lane's start (slots keep offsets relative to it)
   uint32_t cap, n, okn;
   uint64_t okmask, okmask2, ovf;
   __device__ __forceinline__ void operator()(uint64_t p, bool ok, const FlowWords &f) {
     if (n < cap) {
-      if (slot0) {
-        u32x4 r0, r1;
-        row_image(f, p, r0, r1);
-        slot_store(slot0 + (uint64_t)n * 128u, r0);
-        slot_store(slot0 + (uint64_t)n * 128u + 1u, r1);
+      if (slot_a) {
+        u32x4 a;
+        uint32_t b[3];
+        slot_image(f, p, lo, a, b);
+        slot_a[(uint64_t)n * 64u] = a;
+        uint32_t *d = slot_b + (uint64_t)n * 192u;
+        d[0] = b[0];
+        d[1] = b[1];
+        d[2] = b[2];
       }
       if (n < 64) okmask |= (uint64_t)ok << n;
       else okmask2 |= (uint64_t)ok << (n - 64u);
@@ -388,9 +411,12 @@ struct AreaSink {
     okn += ok ? 1u : 0u;
   }
 };
-// slot k of lane l in group g: 32-B row ((g cap + k) 64 + l) of the area
-__device__ __forceinline__ u32x4 *slot_base(const SparseParams &sp, uint64_t g, uint32_t lane) {
-  return sp.kp.flows ? reinterpret_cast<u32x4 *>(sp.area) + ((uint64_t)g * sp.cap * 64u + lane) * 2u : nullptr;
+// the sink of lane l in group g: slot k at r = (g cap + k) 64 + l
+__device__ __forceinline__ AreaSink area_sink(const SparseParams &sp, uint64_t g, uint32_t lane) {
+  const uint64_t r0 = (uint64_t)g * sp.cap * 64u + lane;
+  const bool fl = sp.kp.flows != nullptr;
+  return AreaSink{fl ? reinterpret_cast<u32x4 *>(sp.area) + r0 : nullptr, fl ? sp.area_b + r0 * 3u : nullptr,
+                  lane_lo(sp, g * 64u + lane), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
 }
 
 // one output row (+ the IPv6 side row: its 32 address bytes re-read from the capture)
@@ -459,7 +485,7 @@ __global__ __launch_bounds__(kSpBlock) __attribute__((amdgpu_waves_per_eu(4))) v
     }
   }
   uint32_t cnt = 0;
-  AreaSink sink{slot_base(sp, g, lane), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
+  AreaSink sink = area_sink(sp, g, lane);
   uint64_t exit = 0;
   if (entry != kNone) exit = lane_walk(kp, row, entry, hi, cnt, sink);
   SparseLane L{entry, exit, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
@@ -898,7 +924,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
           const uint32_t b = task[k] >> 6, j = task[k] & 63u, w = bad[b];
           const uint64_t li = (uint64_t)w * 64 + j, p = tpos[k];
           uint32_t cnt = 0;
-          AreaSink sink{slot_base(sp, w, j), sp.cap, 0u, 0u, 0ull, 0ull, kNone};
+          AreaSink sink = area_sink(sp, w, j);
           const uint64_t ex = lane_walk(kp, rows + tid * kSpRow, p, sp_end(sp, (int64_t)li), cnt, sink);
           sp.lanes[li] = SparseLane{p, ex, cnt, sink.okn, sink.ovf, sink.okmask, sink.okmask2};
           ++rw;
@@ -926,32 +952,47 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
 
 // =============================================================================================
 // k_sparse_rows: group w's Ok flows (file order i = 0 .. okw-1, global index O + i) to rows
-// flow_cap - 1 - (O + i).  The group's slots go through LDS kRowChunk slot rows at a time: read
-// as 1-KiB contiguous pieces, written back as each lane's run of consecutive rows (thread 4j + s
-// takes lane j's slots k0 + s + 4m: the four threads of a lane store neighbouring rows).  The next
+// flow_cap - 1 - (O + i).  The group's slots go through LDS kRowChunk slot rows at a time: a slot row
+// is 1 KiB of 16-B slot heads (area) + 768 B of 12-B slot tails (area_b), read as 112 contiguous
+// 16-B chunks, a chunk only when a slot in it holds an Ok flow; written back as each lane's run of
+// consecutive rows (thread 4j + s takes lane j's slots k0 + s + 4m: the four threads of a lane
+// store neighbouring rows), each row's record offset rebuilt from the lane's start.  The next
 // chunk's loads are in flight (registers) while the current one is written; the first chunk's are
 // issued before the lanes' chain walk-through, which wave 0 runs from registers.
 // =============================================================================================
-constexpr uint32_t kRowChunk = 16;  // slot rows (of 64 lanes) per LDS stage: 32 KiB
-constexpr uint32_t kRowPer = kRowChunk * 128u / kSpBlock;  // 16-B slot chunks per thread per stage
+constexpr uint32_t kRowChunk = 16;                       // slot rows (of 64 lanes) per LDS stage: 28 KiB
+constexpr uint32_t kSlotChunks = 64u + 48u;              // 16-B chunks per slot row: heads, then tails
+constexpr uint32_t kHeadPer = kRowChunk * 64u / kSpBlock;  // head chunks per thread per stage (lane tid & 63)
+constexpr uint32_t kTailPer = kRowChunk * 48u / kSpBlock;  // tail chunks per thread per stage
+static_assert(kRowChunk * 64u % kSpBlock == 0 && kRowChunk * 48u % kSpBlock == 0, "whole chunks per thread");
+__device__ __forceinline__ bool bit_k(uint64_t m, uint64_t m2, uint32_t k) {
+  return ((k < 64u ? m >> k : m2 >> (k - 64u)) & 1ull) != 0;
+}
 __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   __shared__ uint32_t opre[65];
   __shared__ uint32_t okl[64], sl[64];  // Ok flows of the lane, in its slots
   __shared__ uint64_t ovf[64], hil[64], msk[64], msk2[64];
   __shared__ uint32_t kmax_sh;
-  __shared__ __attribute__((aligned(16))) u32x4 stage[kRowChunk * 64 * 2];
+  __shared__ __attribute__((aligned(16))) u32x4 stage[kRowChunk * kSlotChunks];
   const ParseParams &kp = sp.kp;
   const uint32_t w = blockIdx.x, tid = threadIdx.x;
   if (__hip_atomic_load(sp.ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != gran(kp.epoch, 1)) return;
-  const u32x4 *area = reinterpret_cast<const u32x4 *>(sp.area) + (uint64_t)w * sp.cap * 128u;
   // the first chunk (slot rows 0 .. 15 of every lane): lanes hold ~40-60 records, so these are
-  // nearly always needed; loaded while wave 0 works out which lanes the chain runs through
-  u32x4 v[kRowPer];
-  const uint32_t n0 = sp.cap < kRowChunk ? sp.cap * 128u : kRowChunk * 128u;  // (the group's slot area: cap rows)
+  // nearly always needed; loaded while wave 0 works out which lanes the chain runs through.
+  // Thread t stages heads of lane t & 63 (slot rows (t >> 6) + 4 u) and tail chunks t + 256 u.
+  const u32x4 *heads = reinterpret_cast<const u32x4 *>(sp.area) + (uint64_t)w * sp.cap * 64u;
+  const u32x4 *tails = reinterpret_cast<const u32x4 *>(sp.area_b + (uint64_t)w * sp.cap * 192u);  // 48 chunks per slot row
+  const uint32_t rows0 = sp.cap < kRowChunk ? sp.cap : kRowChunk;
+  u32x4 vh[kHeadPer], vt[kTailPer];
 #pragma unroll
-  for (uint32_t u = 0; u < kRowPer; ++u) {
+  for (uint32_t u = 0; u < kHeadPer; ++u) {
+    const uint32_t k = (tid >> 6) + 4u * u;
+    vh[u] = k < rows0 ? heads[k * 64u + (tid & 63u)] : u32x4{0u, 0u, 0u, 0u};
+  }
+#pragma unroll
+  for (uint32_t u = 0; u < kTailPer; ++u) {
     const uint32_t q = tid + u * kSpBlock;
-    v[u] = q < n0 ? area[q] : u32x4{0u, 0u, 0u, 0u};
+    vt[u] = q < rows0 * 48u ? tails[q] : u32x4{0u, 0u, 0u, 0u};
   }
   const uint64_t l0 = (uint64_t)w * 64;
   const uint32_t size = sp.nlanes - l0 < 64 ? (uint32_t)(sp.nlanes - l0) : 64u;
@@ -995,29 +1036,37 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
   const uint64_t mj = msk[j], mj2 = msk2[j];
   const uint32_t pj = opre[j];
   const uint32_t c0j = (uint32_t)__builtin_popcountll(mj);  // Ok flows of lane j in slots 0 .. 63
-  // the slots this thread stages are always lane (tid >> 1) & 63's (q = tid + 256 u): a later chunk
-  // loads a slot row's 16-B chunk only when one of the four lanes sharing its 128-B line has an Ok
-  // flow there (C3's rows kernel read 313 MB for 256 MB of slots before)
-  const uint32_t lq = ((tid >> 1) & 63u) & ~3u;
-  const uint64_t lmask = msk[lq] | msk[lq + 1] | msk[lq + 2] | msk[lq + 3];
-  const uint64_t lmask2 = msk2[lq] | msk2[lq + 1] | msk2[lq + 2] | msk2[lq + 3];
+  const uint64_t loj = lane_lo(sp, l0 + j);
+  const uint32_t *stw = reinterpret_cast<const uint32_t *>(stage);
+  const uint64_t mh = msk[tid & 63u], mh2 = msk2[tid & 63u];  // the Ok slots of this thread's head lane
   for (uint32_t k0 = 0; k0 < kmax; k0 += kRowChunk) {
     const uint32_t nk = kmax - k0 < kRowChunk ? kmax - k0 : kRowChunk;
 #pragma unroll
-    for (uint32_t u = 0; u < kRowPer; ++u) {
-      const uint32_t q = tid + u * kSpBlock;
-      if (q < nk * 128u) stage[q] = v[u];
+    for (uint32_t u = 0; u < kHeadPer; ++u) {
+      const uint32_t k = (tid >> 6) + 4u * u;
+      if (k < nk) stage[k * kSlotChunks + (tid & 63u)] = vh[u];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kTailPer; ++u) {
+      const uint32_t q = tid + u * kSpBlock, k = q / 48u;
+      if (k < nk) stage[k * kSlotChunks + 64u + q % 48u] = vt[u];
     }
     __syncthreads();
     const uint32_t k1 = k0 + kRowChunk;
-    if (k1 < kmax) {  // the next chunk's loads, in flight while this one is written
+    if (k1 < kmax) {  // the next chunk's loads (a chunk only when a slot in it holds an Ok flow),
+                      // in flight while this one is written
       const uint32_t nk1 = kmax - k1 < kRowChunk ? kmax - k1 : kRowChunk;
 #pragma unroll
-      for (uint32_t u = 0; u < kRowPer; ++u) {
-        const uint32_t q = tid + u * kSpBlock;
-        const uint32_t kk = k1 + (q >> 7);
-        const bool need = kk < 64u ? ((lmask >> kk) & 1ull) : ((lmask2 >> (kk - 64u)) & 1ull);
-        v[u] = q < nk1 * 128u && need ? area[(uint64_t)k1 * 128u + q] : u32x4{0u, 0u, 0u, 0u};
+      for (uint32_t u = 0; u < kHeadPer; ++u) {
+        const uint32_t k = (tid >> 6) + 4u * u;
+        vh[u] = k < nk1 && bit_k(mh, mh2, k1 + k) ? heads[(k1 + k) * 64u + (tid & 63u)] : u32x4{0u, 0u, 0u, 0u};
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kTailPer; ++u) {
+        const uint32_t q = tid + u * kSpBlock, k = q / 48u, c = q % 48u;
+        const uint32_t l1 = (16u * c) / 12u, l2 = (16u * c + 15u) / 12u;  // the lanes whose tails it holds
+        const bool need = bit_k(msk[l1] | msk[l2], msk2[l1] | msk2[l2], k1 + k);
+        vt[u] = k < nk1 && need ? tails[(k1 + k) * 48u + c] : u32x4{0u, 0u, 0u, 0u};
       }
     }
 #pragma unroll
@@ -1029,8 +1078,12 @@ __global__ __launch_bounds__(kSpBlock) void k_sparse_rows(SparseParams sp) {
                                        : c0j + (uint32_t)__builtin_popcountll(mj2 & ((1ull << (k - 64u)) - 1ull));
         const uint64_t gi = O + pj + below;
         if (gi < kp.flow_cap) {
-          const uint32_t q = ((k - k0) * 64u + j) * 2u;
-          put_row(kp, kp.flow_cap - 1 - gi, stage[q], stage[q + 1]);
+          const uint32_t rk = k - k0;
+          const uint32_t tb = (rk * kSlotChunks + 64u) * 4u + 3u * j;  // the tail's first dword
+          const uint32_t b2 = stw[tb + 2];
+          u32x4 r0, r1;
+          slot_row(stage[rk * kSlotChunks + j], stw[tb], stw[tb + 1], b2, loj + (b2 >> 14), r0, r1);
+          put_row(kp, kp.flow_cap - 1 - gi, r0, r1);
         }
       }
     }
