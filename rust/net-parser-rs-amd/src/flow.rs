@@ -127,20 +127,47 @@ fn convert<'b>(records: Vec<PcapRecord<'b>>, input: Option<&[u8]>) -> Result<Vec
 /// convert_records) fused into one device pass with the PCIe transfers pipelined
 /// (npr_parse_extract_pipelined).  Returns the unparsed remainder and the (record, flow) pairs
 /// in convert_records order.
+/// Rows to reserve for a capture's flows: its record count predicted from the mean size of the
+/// records in its first 256 KiB (the record chain walked on the host, 16 + incl_len each), +1/16
+/// and +64 of slack; one row per 80 B (a 64-B frame) when fewer than 16 records fit there.
+fn rows_for(input: &[u8], big: bool) -> usize {
+    let body = &input[24.min(input.len())..];
+    let head = &body[..body.len().min(256 << 10)];
+    let (mut off, mut n) = (0usize, 0usize);
+    while off + 16 <= head.len() {
+        let b = [head[off + 8], head[off + 9], head[off + 10], head[off + 11]];
+        let incl = if big { u32::from_be_bytes(b) } else { u32::from_le_bytes(b) } as usize;
+        if incl > head.len() - off - 16 {
+            break;
+        }
+        off += 16 + incl;
+        n += 1;
+    }
+    let mean = if n >= 16 { (off / n).max(16) } else { 80 };
+    let est = body.len() / mean + 1;
+    est + est / 16 + 64
+}
+
 pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapRecord<'b>, Flow)>), crate::Error> {
     let (_, header) = crate::GlobalHeader::parse(input)?;
     let big = header.endianness == nom::Endianness::Big;
     let (rows, rows6, consumed) = with_ctx(|ctx| {
-        // Rows for one flow per 80-B record (a 64-B frame and its header: the smallest common
-        // record) first; a capture of smaller records makes the call report NPR_ERR_CAPACITY with
-        // its exact flow count, and it runs once more into exactly that many rows.  (Round 4
-        // reserved one row per 16 B of input, uninitialised: 4x the input in virtual memory,
-        // which a strict-overcommit host refuses)
+        // Rows for the flows the capture's first records predict (rows_for: their mean size over
+        // at most 256 KiB, +1/16 and +64 of slack), uninitialised -- the device writes the Ok
+        // flows' rows right-aligned, and only those are read back, so no zero fill and no
+        // resident pages beyond what the call touches.  A capture whose later records
+        // are smaller makes the call report NPR_ERR_CAPACITY with its exact flow count, and it
+        // runs once more into exactly that many rows.
         let cap_all = input.len().saturating_sub(24) / 16 + 1;
-        let mut cap = (input.len().saturating_sub(24) / 80 + 1).min(cap_all);
+        let mut cap = rows_for(input, big).min(cap_all);
         loop {
-            let mut rows = vec![ffi::npr_flow::default(); cap];
-            let mut rows6 = vec![ffi::npr_flow_v6::default(); cap];
+            let mut rows: Vec<std::mem::MaybeUninit<ffi::npr_flow>> = Vec::with_capacity(cap);
+            let mut rows6: Vec<std::mem::MaybeUninit<ffi::npr_flow_v6>> = Vec::with_capacity(cap);
+            // SAFETY: MaybeUninit elements need no initialisation
+            unsafe {
+                rows.set_len(cap);
+                rows6.set_len(cap);
+            }
             let mut hdr = ffi::npr_global_header::default();
             let (mut n, mut consumed) = (0usize, 0usize);
             let st = unsafe {
@@ -149,8 +176,8 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
                     input.as_ptr(),
                     input.len(),
                     &mut hdr,
-                    rows.as_mut_ptr(),
-                    rows6.as_mut_ptr(),
+                    rows.as_mut_ptr() as *mut ffi::npr_flow,
+                    rows6.as_mut_ptr() as *mut ffi::npr_flow_v6,
                     cap,
                     &mut n,
                     &mut consumed,
@@ -162,14 +189,21 @@ pub fn parse_and_convert<'b>(input: &'b [u8]) -> Result<(&'b [u8], Vec<(PcapReco
                 continue;
             }
             check(ctx, st)?;
-            // right-aligned: rows[cap - k .. cap] in convert_records order (a side row only where
-            // the flow is IPv6: the others are taken as zero)
+            // right-aligned: rows[cap - k .. cap] in convert_records order, written by the call;
+            // a side row is written (and read) only where the flow is IPv6
             let k = n.min(cap);
-            let tail: Vec<ffi::npr_flow> = rows[cap - k..cap].to_vec();
+            // SAFETY: the call wrote rows[cap - k .. cap], and side rows of IPv6 flows among them
+            let tail: Vec<ffi::npr_flow> = rows[cap - k..cap].iter().map(|r| unsafe { r.assume_init_read() }).collect();
             let tail6: Vec<ffi::npr_flow_v6> = rows6[cap - k..cap]
                 .iter()
                 .zip(tail.iter())
-                .map(|(f6, f)| if f.kind & ffi::NPR_FLOW_KIND_IPV6 != 0 { *f6 } else { ffi::npr_flow_v6::default() })
+                .map(|(f6, f)| {
+                    if f.kind & ffi::NPR_FLOW_KIND_IPV6 != 0 {
+                        unsafe { f6.assume_init_read() }
+                    } else {
+                        ffi::npr_flow_v6::default()
+                    }
+                })
                 .collect();
             return Ok((tail, tail6, consumed));
         }
