@@ -39,7 +39,8 @@
 // launch, launch gaps included, like bench.py's kernel_ms); run under rocprofv3 --kernel-trace
 // --stats for kernel durations.
 // Build: hipcc -O3 --offload-arch=gfx950 scripts/microbench/rw_floor.hip -o scripts/microbench/rw_floor
-// Usage: rw_floor [S] [sweep|lookback|all]
+// Usage: rw_floor [S] [sweep|lookback|all|floor] [capture bytes (default 80000024)]
+//   floor: R, L and P at W = 32 only (e.g. the per-record convert's bytes: 88 or 120 MB read)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -377,7 +378,8 @@ int main(int argc, char **argv) {
   const char *what = argc > 2 ? argv[2] : "all";
   const bool sweep = !strcmp(what, "sweep") || !strcmp(what, "all");
   const bool look = !strcmp(what, "lookback") || !strcmp(what, "all");
-  const uint64_t len = 80000024;
+  const bool floor_only = !strcmp(what, "floor");
+  const uint64_t len = argc > 3 ? strtoull(argv[3], nullptr, 10) : 80000024ull;
   const uint32_t ntiles = (uint32_t)((len + kTile - 1) / kTile);
   hipDeviceProp_t prop;
   CK(hipGetDeviceProperties(&prop, 0));
@@ -433,9 +435,9 @@ int main(int argc, char **argv) {
   const double rb = (double)len;
   auto rep = [&](const char *name, uint32_t wbytes, float us, double r) {
     const double w = (double)ntiles * kRowsPerTile * wbytes;
-    printf("%-62s W=%2u %7.2f us  read %6.0f GB/s (read-only frac %.3f)  total %6.0f GB/s  frac(112MB) %.3f\n", name,
-           wbytes, us, r / (us * 1e-6) / 1e9, r / (us * 1e-6) / 8e12, (r + w) / (us * 1e-6) / 1e9,
-           112000024.0 / (us * 1e-6) / 8e12);
+    printf("%-62s W=%2u %7.2f us  read %6.0f GB/s (read-only frac %.3f)  total %6.0f GB/s  frac(read+32B rows) %.3f\n",
+           name, wbytes, us, r / (us * 1e-6) / 1e9, r / (us * 1e-6) / 8e12, (r + w) / (us * 1e-6) / 1e9,
+           (rb + (double)ntiles * kRowsPerTile * 32) / (us * 1e-6) / 8e12);
   };
 #define RUN(M, WB, name, r)                                                                                  \
   mode_now = M;                                                                                              \
@@ -443,6 +445,11 @@ int main(int argc, char **argv) {
   rep(name, WB, timeit([&](int i) { hipLaunchKernelGGL(k_rw<M>, dim3(nwg), dim3(kWg * 64), 0, 0, arg(i)); }, S), r)
   for (int round = 0; round < 3; ++round) {
     printf("-- round %d\n", round);
+    if (floor_only) {
+      RUN('R', 0, "R read only", rb);
+      RUN('L', 32, "L rows after the wave's own range (others still read)", rb);
+      RUN('P', 32, "P 8-B granule per line, atomic polls", rb);
+    }
     if (sweep) {
       RUN('R', 0, "R read only", rb);
       for (uint32_t wb : {32u, 16u, 8u}) {
