@@ -772,7 +772,7 @@ static npr_status sparse_launch(npr_ctx *c, npr::ParseParams &p, const npr_summa
   npr::SparseParams sp{};
   const uint64_t range = p.stop > p.start ? p.stop - p.start : 0;
   sp.span = std::min<uint64_t>(span, npr::kSparseSpanMax);  // (a slot keeps 18 bits of record offset)
-  sp.nlanes = (range + span - 1) / span;
+  sp.nlanes = (range + sp.span - 1) / sp.span;  // (lanes of the clamped span cover the range)
   const uint64_t ng = (sp.nlanes + 63) / 64;
   if (ng > 0x7fffffffull) return fail(c, NPR_ERR_ARG, "input too large for the sparse walk");
   sp.ngroups = (uint32_t)ng;

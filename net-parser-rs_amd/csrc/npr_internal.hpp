@@ -71,6 +71,7 @@ enum : uint32_t {
   kStatMismWait = 1,   // prefixes that waited for a mis-speculated tile's exact prefix
   kStatFoldSlow = 2,   // pass-1 group folds that took the serial (inconsistent-link) path
   kStatScanRounds = 3, // sparse scan: resolve rounds (0 when the fast path settles every link)
+  kStatQueueFull = 4,  // sparse resolve passes whose shared re-walk queue overflowed (tasks deferred)
   kStatNoEntry = 5,    // tiles with no plausible record start
   kStatCount = 8
 };

@@ -621,7 +621,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
   __shared__ uint32_t wsn[kScanThreads / 64 + 1];
   __shared__ Seg badx[kResolvers];
   __shared__ uint32_t bad[kResolvers];
-  __shared__ uint32_t nbad, first_w, fail, rewalks;
+  __shared__ uint32_t nbad, first_w, fail, rewalks, qfull;
   __shared__ uint64_t entry0;
   __shared__ Seg E0, TOT;
   __shared__ uint32_t rows[kResolvers * kSpRow];
@@ -642,6 +642,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
     first_w = ~0u;
     fail = 0;
     rewalks = 0;
+    qfull = 0;
   }
   __syncthreads();
   if ((kp.flags & kFlagSpecStart) && !kp.prev)  // the anchor: the first lane entry found
@@ -852,6 +853,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
         sm->entry = entry0;
         __hip_atomic_store(sp.ctl, gran(kp.epoch, 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (kp.stats && rewalks) atomicAdd(kp.stats + kStatRewalk, rewalks);
+        if (kp.stats && qfull) atomicAdd(kp.stats + kStatQueueFull, qfull);
         if (kp.stats) atomicAdd(kp.stats + kStatScanRounds, round + 1);
       }
       return;
@@ -919,6 +921,7 @@ __global__ __launch_bounds__(kScanThreads) void k_sparse_scan(SparseParams sp) {
         fence_agent();
         const uint32_t nt = ntask < kTasks - 64u ? 64u + ntask : kTasks;
         if (ntask == 0 && npass == 0) break;
+        if (tid == 0 && ntask > kTasks - 64u) ++qfull;
         for (uint32_t k = tid; k < nt; k += kScanThreads) {  // (b) every thread re-walks tasks
           if (task[k] == ~0u) continue;  // an unclaimed reserved slot
           const uint32_t b = task[k] >> 6, j = task[k] & 63u, w = bad[b];

@@ -7,6 +7,7 @@ synthetic captures (net_parser_rs.synth) sized so the oracle finishes in seconds
 reference's own KAT frames.  Full-size configs (C2 1M, C3 8M, C4 16M/64M, the C5 tiled corpus) are
 checked bit-exact or per shard in test_gpu_scale.py.
 """
+import ctypes
 import json
 import os
 import struct
@@ -222,6 +223,37 @@ def test_adversarial_speculation(light):
 @LIGHT
 def test_jumbo_records_span_many_tiles(light):
     check_parity(synth.quirk_corpus(600, seed=6, jumbo_every=2), light=light)
+
+
+@pytest.mark.parametrize("span", [1 << 20, 4 << 20])
+@pytest.mark.parametrize("corpus", ["jumbo", "c3"])
+def test_sparse_lane_ranges_past_the_slot_offset_limit(corpus, span):
+    """A sparse slot keeps its record offset as 18 bits relative to the lane start, so lane ranges
+    are capped at 256 KiB (npr_internal.hpp kSparseSpanMax): larger forced ranges run at the cap,
+    with the same results (jumbo records of 20-70 KB, and C3-like records)."""
+    blob = {"jumbo": lambda: synth.quirk_corpus(900, seed=66, jumbo_every=2),
+            "c3": lambda: synth.variable_mix(60_000)}[corpus]()
+    check_parity(blob, light=f"sparse_s{span}")
+
+
+@pytest.mark.parametrize("span", [128, 256])
+def test_sparse_resolve_queue_overflow(span):
+    """Fake record-header chains in every other payload under short lane ranges: most lanes
+    mis-speculate, so a resolve pass queues more re-walks than the 2048-task shared queue holds (the
+    rest wait for the next pass; stats counter [4] counts such passes).  Results stay the serial
+    chain's."""
+    blob = synth.quirk_corpus(40_000, seed=67, fake_every=2)
+    ctx = npr.context(0)
+    lib, h = ctx.lib, ctx.handle
+    st = (ctypes.c_uint32 * 8)()
+    ctx.check(lib.npr_ctx_set_stats(h, 1))
+    ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))  # (zero the counters)
+    try:
+        check_parity(blob, light=f"sparse_s{span}")
+        ctx.check(lib.npr_ctx_read_stats(h, st, 8, 1))
+    finally:
+        ctx.check(lib.npr_ctx_set_stats(h, 0))
+    assert st[0] > 2048 and st[4] > 0, list(st)
 
 
 @LIGHT
