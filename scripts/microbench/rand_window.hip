@@ -10,6 +10,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                  \
@@ -124,6 +125,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   atomicAdd(out + 2, (unsigned long long)acc);
 }
 
+// Persistent waves over small lane ranges in address order: wave w takes groups w, w + W, ... (64
+// lanes of `span` bytes each), so at any moment the waves work inside one band of W x 64 x span
+// bytes of the buffer instead of across all of it (the walk's lanes all start at once, spread over
+// the whole capture).  SPEC: each lane first loads three dependent windows (the walk's start
+// speculation: a screening window and two chained headers) before its chain.
+template <int SPEC>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_band(const uint8_t *buf, uint64_t span,
+                                                                                       uint64_t nlanes, unsigned long long *out) {
+  const uint64_t nw = (uint64_t)gridDim.x * 4u, w = (uint64_t)blockIdx.x * 4u + (threadIdx.x >> 6);
+  const uint32_t lane = threadIdx.x & 63u;
+  uint32_t acc = 0, n = 0, lines = 0;
+  for (uint64_t g = w; g * 64 < nlanes; g += nw) {
+    const uint64_t l = g * 64 + lane;
+    if (l >= nlanes) continue;
+    uint64_t pos = l * span;
+    const uint64_t hi = pos + span;
+    if (SPEC) {
+      uint32_t w0;
+      acc += win_sum(buf, pos, w0);
+      uint64_t q = pos + 16u + (w0 % 61u);
+      acc += win_sum(buf, q, w0);
+      q += 16u + 64u + (w0 % 1441u);
+      acc += win_sum(buf, q, w0);
+      lines += lines_of(pos) + 2;
+      acc += (uint32_t)q;
+    }
+    while (pos < hi) {
+      uint32_t w0;
+      acc += win_sum(buf, pos, w0);
+      lines += lines_of(pos);
+      ++n;
+      pos += 16u + 64u + (w0 % 1441u);
+    }
+  }
+  atomicAdd(out, (unsigned long long)n);
+  atomicAdd(out + 1, (unsigned long long)lines);
+  atomicAdd(out + 2, (unsigned long long)acc);
+}
+
 int main(int argc, char **argv) {
   const uint64_t bytes = 6400ull << 20;
   const uint64_t nlanes = argc > 1 ? strtoull(argv[1], 0, 0) : 160000ull;
@@ -144,14 +184,16 @@ int main(int argc, char **argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const dim3 grid((unsigned)((nlanes + 255) / 256));
+  const dim3 grid0((unsigned)((nlanes + 255) / 256));
+  dim3 grid = grid0;
+  uint64_t span_run = span, nl_run = nlanes;
   auto run = [&](const char *name, void (*k)(const uint8_t *, uint64_t, uint64_t, unsigned long long *)) {
     float best = 1e30f;
     unsigned long long r[3] = {0, 0, 0};
     for (int it = 0; it < 4; ++it) {
       CK(hipMemset(out, 0, sizeof(r)));
       CK(hipEventRecord(e0));
-      hipLaunchKernelGGL(k, grid, dim3(256), 0, 0, buf, span, nlanes, out);
+      hipLaunchKernelGGL(k, grid, dim3(256), 0, 0, buf, span_run, nl_run, out);
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
@@ -160,10 +202,30 @@ int main(int argc, char **argv) {
       CK(hipMemcpy(r, out, sizeof(r), hipMemcpyDeviceToHost));
     }
     printf("%-9s lanes %llu  %.3f ms  windows %.2fM  lines %.2fM (%.2f/window)  %.1f G lines/s  %.2f TB/s of lines\n", name,
-           (unsigned long long)nlanes, best, r[0] / 1e6, r[1] / 1e6, (double)r[1] / r[0], r[1] / (best * 1e-3) / 1e9,
+           (unsigned long long)nl_run, best, r[0] / 1e6, r[1] / 1e6, (double)r[1] / r[0], r[1] / (best * 1e-3) / 1e9,
            r[1] * 128.0 / (best * 1e-3) / 1e12);
     fflush(stdout);
   };
+  if (argc > 2 && std::string(argv[2]) == "band") {
+    // persistent 1024 workgroups (4 per CU) over lanes of S bytes for S in the list
+    grid = dim3(1024);
+    for (uint64_t S : {4096ull, 8192ull, 16384ull, 40960ull}) {
+      span_run = S;
+      nl_run = (bytes - 4096) / S;
+      char nm[64];
+      snprintf(nm, sizeof nm, "band%llu", (unsigned long long)S);
+      run(nm, k_band<0>);
+      snprintf(nm, sizeof nm, "band%llu+spec", (unsigned long long)S);
+      run(nm, k_band<1>);
+    }
+    grid = grid0;
+    span_run = span;
+    nl_run = nlanes;
+    run("chain1", k_chain<1>);
+    CK(hipFree(buf));
+    CK(hipFree(out));
+    return 0;
+  }
   run("chain1", k_chain<1>);
   run("chain2", k_chain<2>);
   run("chain1+slots", k_chain<1, 1>);
