@@ -212,7 +212,8 @@ def stats_dump(ws, bufs, hdr, copies, rank):
         ws.ctx.check(lib.npr_ctx_read_stamps(h, stamps.ctypes.data, stamps.size, ctypes.byref(ntl)))
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
         np.save(os.path.join(REPO, "gpurun_out", f"stamps_rank{rank}.npy"), stamps.reshape(nt, 16))
-    print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} tiles={nt}", file=sys.stderr, flush=True)
+    print(f"[rank {rank}] stats rewalk={st[0]} mism_wait={st[1]} none={st[5]} lookback_rereads={st[6]} tiles={nt}",
+          file=sys.stderr, flush=True)
     ws.ctx.check(lib.npr_ctx_set_stats(h, 0))
 
 

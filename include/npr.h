@@ -216,8 +216,9 @@ npr_status npr_stream_release(npr_ctx *ctx, void *stream);
  * Counters: [0] tiles pass 2 re-walked (pass 1's entry was not the exact one), [1] prefix folds
  * that waited for a mis-speculated tile's exact prefix, [3] sparse-walk scan rounds (resolving
  * contradicted lane groups), [4] sparse resolve passes whose shared re-walk queue was full (tasks
- * deferred to the next pass), [5] tiles with no plausible record start; the others are reserved
- * (0).  In the sparse walk [0] counts lane re-walks. */
+ * deferred to the next pass), [5] tiles with no plausible record start, [6] (stats mode 2 only)
+ * resident look-back re-read rounds summed over workgroups; [7] is reserved (0).  In the sparse
+ * walk [0] counts lane re-walks. */
 npr_status npr_ctx_set_stats(npr_ctx *ctx, int enable);
 npr_status npr_ctx_read_stats(npr_ctx *ctx, uint32_t *out, int n, int reset);
 /* With npr_ctx_set_stats(ctx, 2): s_memrealtime (100 MHz) stamps of the last parse, 16 words

@@ -73,6 +73,7 @@ enum : uint32_t {
   kStatScanRounds = 3, // sparse scan: resolve rounds (0 when the fast path settles every link)
   kStatQueueFull = 4,  // sparse resolve passes whose shared re-walk queue overflowed (tasks deferred)
   kStatNoEntry = 5,    // tiles with no plausible record start
+  kStatLbPolls = 6,    // resident look-back re-read rounds, summed over workgroups (DIAG kernels only)
   kStatCount = 8
 };
 constexpr int kStampWords = 16;  // diagnostic stamps per tile (npr_ctx_read_stamps)

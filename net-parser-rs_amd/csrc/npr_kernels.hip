@@ -1770,7 +1770,8 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
     // every window at once: re-read (returning atomics) only the aggregates not yet this
     // launch's -- not published yet, or a line an earlier launch left in this XCD's L2
     uint32_t nap = 1;
-    for (int tries = 0;; ++tries) {
+    int tries = 0;
+    for (;; ++tries) {
       bool miss = false;
 #pragma unroll
       for (int w = 0; w < kTopWin; ++w) {
@@ -1793,6 +1794,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
       }
     }
     if (DIAG) stamp_at(st, 13);
+    if (DIAG && kp.stats && lane == 0 && tries) atomicAdd(kp.stats + kStatLbPolls, (uint32_t)tries);
     if (kp.prev) {  // a chained launch: the chain continues where the previous one left it
       const uint64_t pc = kp.prev->consumed, pr = kp.prev->n_records, pf = kp.prev->n_flows;
       okw = okw && (kp.prev_epoch == 0 || kp.prev->epoch == kp.prev_epoch);  // it completed
