@@ -207,8 +207,9 @@ int main(int argc, char **argv) {
     fflush(stdout);
   };
   if (argc > 2 && std::string(argv[2]) == "band") {
-    // persistent 1024 workgroups (4 per CU) over lanes of S bytes for S in the list
-    grid = dim3(1024);
+    // persistent workgroups of 4 waves (argv[3]: how many; 1024 = 4 per CU) over lanes of S bytes
+    grid = dim3(argc > 3 ? (unsigned)strtoul(argv[3], 0, 0) : 1024u);
+    printf("persistent workgroups: %u (%u waves)\n", grid.x, grid.x * 4u);
     for (uint64_t S : {4096ull, 8192ull, 16384ull, 40960ull}) {
       span_run = S;
       nl_run = (bytes - 4096) / S;
