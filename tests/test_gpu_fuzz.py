@@ -150,3 +150,56 @@ def test_unmutated_splice_every_shape(case):
     blob = base_capture(rng)
     for shape in SHAPES:
         run_shape(rng, blob, shape)
+
+
+# ---- the other entry points over mutated captures ----------------------------------------------
+@pytest.mark.parametrize("case", range(24))
+def test_mutated_records_api(case):
+    """npr_dev_extract_flows / npr_dev_convert_records over the parsed records of a mutated capture,
+    some payloads shrunk to a prefix, the list permuted on odd cases."""
+    from test_gpu_records_api import check_convert, check_dense, records_of
+    rng = np.random.default_rng(0xA91 + case)
+    blob = mutate(rng, base_capture(rng))
+    recs = records_of(blob, shrink=float(rng.choice([0.0, 0.2, 0.7])), permute=bool(case & 1), seed=case)
+    check_dense(blob, recs)
+    check_convert(blob, recs, cap=None if case % 3 else max(1, len(recs) // 2))
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_mutated_host_pipelined(case):
+    """npr_parse_extract_pipelined (chunked H2D, chained links, per-link D2H) and, on odd cases, its
+    bounded device window, over mutated captures at random chunk sizes."""
+    from test_gpu_host_stream import check_pipelined, check_windowed
+    rng = np.random.default_rng(0x91BE + case)
+    blob = mutate(rng, base_capture(rng))
+    chunk = int(rng.choice([65536, 100_000, 1 << 19]))
+    if case & 1:
+        check_windowed(blob, max(chunk, 1 << 16), int(rng.choice([3, 4, 7])))
+    else:
+        check_pipelined(blob, chunk, pinned=bool(case & 2))
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_mutated_shards_in_process(case):
+    """Record-range shards of a mutated capture (the multi-GPU path's per-rank launches and summary
+    replay, in one process), merged and compared with the serial oracle."""
+    import torch
+
+    from net_parser_rs import _abi, device, parallel
+    rng = np.random.default_rng(0x54A2D + case)
+    blob = mutate(rng, base_capture(rng))
+    rc, hdr, recs, cons = _oracle.capture_file_parse(blob)
+    flows, v6 = _oracle.convert_records(blob, recs)
+    t = torch.empty(len(blob), dtype=torch.uint8, device="cuda")
+    t.copy_(torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()))
+    ws = device.Workspace(len(recs) + 1, len(recs) + 1, records=False)
+    local = parallel.device_local(ws, t, len(blob), endianness=hdr.endianness)
+    world = int(rng.integers(2, 9))
+    results, live, rounds = parallel.parse_sharded_inprocess(local, 24, len(blob), world)
+    _, _, r_tot, f_tot = parallel.prefix_offsets(results, live)
+    assert (r_tot, f_tot) == (len(recs), len(flows))
+    merged, merged6 = parallel.merge_flows(results, live)
+    assert merged.tobytes() == flows.tobytes()
+    m = (flows["kind"] & _abi.KIND_IPV6) != 0
+    if m.any():
+        assert merged6[m].tobytes() == v6[m].tobytes()
