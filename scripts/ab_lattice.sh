@@ -1,5 +1,6 @@
 #!/bin/bash
-# Interleaved C2 timing of the product library with lattice rows on and off (NPR_NO_LATTICE=1):
+# Interleaved C2 timing of the round-6 lattice-rows experiment build (scripts/variants/r6_lattice_rows.diff
+# applied; NPR_NO_LATTICE=1 switched it off there -- the product has no such switch), on and off:
 # ROUNDS x each, bench.py --steps 200 (HIP-event kernel time printed).  Usage: ab_lattice.sh TAG ROUNDS
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"; mkdir -p gpurun_out
