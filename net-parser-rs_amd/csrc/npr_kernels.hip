@@ -1206,7 +1206,7 @@ __device__ __forceinline__ Seg res_prefix_seg(const ParseParams &kp, uint64_t *e
 
 // exact chain state before wave v, from X = E(b) ⊕ (prefix inside the workgroup) when that is
 // flagged: contradictions settled by exact prefixes P(m), then aggregates (G(b) where aligned)
-__device__ __forceinline__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t0) {
+__device__ __forceinline__ bool res_prefix(const ParseParams &kp, uint32_t v, Seg &X, uint64_t t0, const Seg *own_a) {
   const uint32_t lane = threadIdx.x & 63u;
   if (X.valid) return true;
   // a mis-speculated range m < v: from its exact prefix on, aggregates (G1 where aligned)
@@ -1245,7 +1245,25 @@ __device__ __forceinline__ bool res_prefix(const ParseParams &kp, uint32_t v, Se
         a += take * kResWg;
       } else {
         const uint32_t to_grp = kResWg - a % kResWg, cnt = v - a < to_grp ? v - a : to_grp;
-        if (!res_fold(kp, 0, a, (int)cnt, Y, t0)) return false;
+        if (a / kResWg == v / kResWg) {  // this workgroup's waves: their A's are in its LDS
+          const uint32_t idx = a + cnt - 1u - lane;  // (descending, as res_fold)
+          LaneSeg L{};
+          L.mism = -1;
+          L.valid = true;
+          if (lane < cnt) {
+            const Seg &A = own_a[idx % kResWg];
+            L.entry = A.entry;
+            L.exit = A.exit;
+            L.cnt = A.cnt;
+            L.ok = A.ok;
+            L.first = A.first;
+            L.last = A.last;
+            L.present = true;
+          }
+          Y = fold_window(kp, L, (int)cnt - 1);
+        } else if (!res_fold(kp, 0, a, (int)cnt, Y, t0)) {  // (a workgroup that published its A's)
+          return false;
+        }
         a += cnt;
       }
       X = combine(kp, X, Y);
@@ -1710,16 +1728,6 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
   }
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   __syncthreads();
-  // A in HBM, for the rare generic prefix of another range (its readers wait for the epoch tags).
-  // Stored after the barrier: the barrier's release fence waits for every store issued before it,
-  // and write-through stores held the workgroup's fold back by their round trip.
-  if (active && lane == 0) {
-    RangeSlot *rs = kp.rslots + v;
-    st_agent(&rs->a[0], gran(ep, pos == kNone ? 0ull : pos));
-    st_agent(&rs->a[1], gran(ep, entry == kNone ? 0ull : entry + 1));
-    st_agent(&rs->a[2], gran(ep, cnt));
-    st_agent(&rs->a[3], gran(ep, okc));
-  }
   if (wid == 0) {
     // Wave 0 folds for the whole workgroup.  The rings are idle until the barrier below: its kept
     // flows wait there (stashed right after the publication, which does not wait for it), so the
@@ -1813,8 +1821,20 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
       E = combine(kp, E, fold_window(kp, G[w], (int)(b - w0 < 64u ? b - w0 : 64u) - 1));
     }
     if (DIAG) stamp_at(st, 14);
-    // (3) each wave's prefix
-    if ((uint32_t)lane < nw) sh.x[lane] = lane == 0 ? E : combine(kp, E, e);
+    // (3) each wave's prefix.  A workgroup with a wave whose chain is not the exact one (or whose
+    // prefix is not settled) publishes its waves' A's, for the generic prefixes of the waves above
+    // it (res_prefix: from the mis-speculated wave's exact prefix P(m) on, folding A's of m's
+    // workgroup); with every chain exact nothing reads them, and no wave stores them.
+    const Seg Xl = lane == 0 ? E : combine(kp, E, e);
+    if ((uint32_t)lane < nw) sh.x[lane] = Xl;
+    if (__ballot((uint32_t)lane < nw && (!Xl.valid || Xl.exit != sh.a[lane].entry)) && (uint32_t)lane < nw) {
+      const Seg &A = sh.a[lane];
+      RangeSlot *rs = kp.rslots + b * kResWg + lane;
+      st_agent(&rs->a[0], gran(ep, A.exit));
+      st_agent(&rs->a[1], gran(ep, A.entry == kNone ? 0ull : A.entry + 1));
+      st_agent(&rs->a[2], gran(ep, A.cnt));
+      st_agent(&rs->a[3], gran(ep, A.ok));
+    }
     if (lane == 0) {
       sh.fail = okw ? 0u : 1u;
       if (b == nb - 1) kp.summary->entry = entry0;
@@ -1836,7 +1856,9 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
 
   // ---- phase B ------------------------------------------------------------------------------
   Seg X = sh.x[wid];
-  if (!X.valid && !res_prefix(kp, v, X, t0)) return false;
+  // (a wave whose prefix is settled and continues its chain exactly is nobody's P(m))
+  const bool publish_p = !X.valid || X.exit != entry;
+  if (!X.valid && !res_prefix(kp, v, X, t0, sh.a)) return false;
   if (DIAG) stamp_at(st, 4);
   const uint64_t range_lo = base, range_hi = tile_end(kp, (int64_t)c1 - 1);
   uint64_t xe = uni64(X.exit), xc = uni64(X.cnt), xo = uni64(X.ok);
@@ -1859,10 +1881,12 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
     }
   }
   if (lane == 0) {
-    RangeSlot *rs = kp.rslots + v;
-    st_agent(&rs->p[0], gran(ep, xe));
-    st_agent(&rs->p[1], gran(ep, xc));
-    st_agent(&rs->p[2], gran(ep, xo));
+    if (publish_p) {
+      RangeSlot *rs = kp.rslots + v;
+      st_agent(&rs->p[0], gran(ep, xe));
+      st_agent(&rs->p[1], gran(ep, xc));
+      st_agent(&rs->p[2], gran(ep, xo));
+    }
     if (v == kp.nwaves - 1) {
       uint32_t fl2 = 0;
       if (kp.flows && xo > kp.flow_cap) fl2 |= NPR_SUMMARY_FLOW_OVERFLOW;
