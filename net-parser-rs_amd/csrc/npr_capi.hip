@@ -1093,6 +1093,8 @@ static npr_status grow_events(npr_ctx *c, std::vector<hipEvent_t> &v, uint64_t n
   return NPR_OK;
 }
 
+constexpr size_t kRegisterMin = 1u << 20;  // caller buffers registered for a pipelined call: at least this size
+
 // Is [p, p + n) page-locked host memory (hipHostMalloc'ed or registered)?
 static bool host_pinned(const void *p, size_t n) {
   hipPointerAttribute_t a;
@@ -1254,18 +1256,28 @@ npr_status npr_parse_extract_pipelined(npr_ctx *c, const uint8_t *in, size_t len
   const uint64_t shift = flow_cap - fcap;
   npr_flow *hout = out + shift;
   npr_flow_v6 *hout6 = out_v6 ? out_v6 + shift : nullptr;
-  // the caller's buffers: page-locked for the DMA engines (registered for this call unless they are)
-  struct Unreg {  // unregister on every exit path
+  // the caller's buffers: page-locked for the DMA engines (registered for this call unless they
+  // are).  Buffers under 1 MiB stay pageable (HIP stages them): a small heap buffer shares its pages
+  // with other objects and with the call's other small buffers, and registering such page-sharing
+  // ranges is where a later pageable D2H copy in the same process once failed with
+  // hipErrorIllegalAddress (round 6); small copies gain nothing from pinning anyway
+  struct Unreg {  // unregister on every exit path, and let the runtime finish releasing them before
+                  // the caller may free (and the allocator reuse) the memory
     void *p[3] = {nullptr, nullptr, nullptr};
     ~Unreg() {
+      bool any = false;
       for (void *q : p)
-        if (q) (void)hipHostUnregister(q);
+        if (q) {
+          (void)hipHostUnregister(q);
+          any = true;
+        }
+      if (any) (void)hipDeviceSynchronize();
     }
   } unreg;
   const void *bufs[3] = {in, hout, hout6};
   const size_t sizes[3] = {len, fcap * sizeof(npr_flow), hout6 ? fcap * sizeof(npr_flow_v6) : 0};
   for (int i = 0; i < 3; ++i) {
-    if (!sizes[i] || host_pinned(bufs[i], sizes[i])) continue;
+    if (sizes[i] < kRegisterMin || host_pinned(bufs[i], sizes[i])) continue;
     const hipError_t r = hipHostRegister((void *)bufs[i], sizes[i], hipHostRegisterDefault);
     if (r == hipErrorHostMemoryAlreadyRegistered) {
       (void)hipGetLastError();
