@@ -124,6 +124,19 @@ def test_pipelined_host_parse_pinned_buffers(corpus):
     check_pipelined(CORPORA[corpus](), 65536, pinned=True)
 
 
+def test_tiny_pipelined_calls_then_pageable_copies():
+    """Round 6: many pipelined calls on tiny captures (their capture and row arrays
+    are small heap objects sharing pages), then host-path parses that copy rows into fresh pageable
+    arrays; every result against the oracle."""
+    base = synth.quirk_corpus(40, seed=81)
+    rc, hdr, recs, cons = _oracle.capture_file_parse(base)
+    for k in range(64):
+        cut = int(recs["offset"][k % len(recs)]) + 16 + (k % 7)
+        check_pipelined(base[:max(cut, 25)], 65536, pinned=False)
+    for seed in (82, 83):
+        check_host(synth.quirk_corpus(20_000, seed=seed), 0)
+
+
 def test_pipelined_c2_x4_320mb():
     """The measured configuration: 4M C2 records, 32 MiB chunks, bit-exact."""
     check_pipelined(synth.fixed64(4_000_000), 0, pinned=True)
