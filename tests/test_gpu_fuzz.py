@@ -203,3 +203,27 @@ def test_mutated_shards_in_process(case):
     m = (flows["kind"] & _abi.KIND_IPV6) != 0
     if m.any():
         assert merged6[m].tobytes() == v6[m].tobytes()
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_mutated_batches(case):
+    """npr_dev_parse_extract_batch over 2-9 mutated captures of mixed shapes and byte orders."""
+    from test_gpu_batch import run_batch
+    rng = np.random.default_rng(0xBA7C + case)
+    run_batch([mutate(rng, base_capture(rng)) for _ in range(int(rng.integers(2, 10)))])
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_mutated_flow_table(case):
+    """Row f4 (the distinct-flow table) over the flow table of a mutated capture, with random
+    weights and, on odd cases, an output capacity below the distinct count."""
+    import torch
+
+    from test_gpu_flowtable import check, device_table
+    rng = np.random.default_rng(0xF70 + case)
+    blob = mutate(rng, base_capture(rng))
+    fl, f6, n = device_table(blob)
+    if n == 0:
+        return
+    w = torch.from_numpy(rng.integers(1, 1000, size=n, dtype=np.uint64).astype(np.int64)).cuda()
+    check(fl, f6, n, weights=w, cap=max(1, n // 3) if case & 1 else None)
