@@ -227,3 +227,14 @@ def test_mutated_flow_table(case):
         return
     w = torch.from_numpy(rng.integers(1, 1000, size=n, dtype=np.uint64).astype(np.int64)).cuda()
     check(fl, f6, n, weights=w, cap=max(1, n // 3) if case & 1 else None)
+
+
+@pytest.mark.parametrize("case", range(8))
+def test_mutated_vxlan(case):
+    """Row f3: VXLAN inner flows over the records of a mutated VXLAN (or other) capture."""
+    from test_vxlan import _check_device
+    rng = np.random.default_rng(0x4789 + case)
+    blob = mutate(rng, synth.vxlan_corpus(int(rng.integers(200, 3000)), seed=int(rng.integers(1, 1 << 30)))
+                  if case % 4 else base_capture(rng))
+    if len(_oracle.capture_file_parse(blob)[2]):
+        _check_device(blob, int(rng.choice([0, 4789, 8472])), bool(case & 1))
