@@ -888,6 +888,11 @@ static npr_status launch_range(npr_ctx *c, const void *input, uint64_t len, uint
     uint64_t wv = std::min<uint64_t>(nt, c->res_waves);
     if (c->resident > 1) wv = std::min<uint64_t>(wv, (uint64_t)c->resident);
     p.nwaves = (uint32_t)wv;
+    if (wv % npr::kResWgMin == 0) {  // per workgroup, then per wave (res_range)
+      const uint64_t nwg = wv / npr::kResWgMin;
+      p.wg_q = (uint32_t)(nt / nwg);
+      p.wg_r = (uint32_t)(nt % nwg);
+    }
     p.rslots = (npr::RangeSlot *)c->slots.p;
     p.rgroups = p.groups[1];
     p.pack = c->res_pack ? 1u : 0u;

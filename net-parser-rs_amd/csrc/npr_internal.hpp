@@ -112,6 +112,9 @@ struct ParseParams {
   uint64_t *stamps;        // diagnostic per-tile s_memrealtime stamps [ntiles][kStampWords] or NULL
   // resident single pass (flows-only launches): 0 = use the two-pass kernels
   uint32_t nwaves;         // persistent waves, each owning a contiguous tile range (<= kResMaxWaves, <= ntiles)
+  // whole workgroups (nwaves a multiple of 16): tiles dealt per workgroup first (wg_q each, one more
+  // for the first wg_r), then over its 16 waves (the oldest take the extra tiles); wg_q == 0: per wave
+  uint32_t wg_q, wg_r;
   RangeSlot *rslots;       // [nwaves]
   GroupSlot *rgroups;      // workgroup aggregates G(b), [ceil(nwaves / kResWg)]
   uint32_t *rcnt;          // pacing counter word (res_arrive; never read)

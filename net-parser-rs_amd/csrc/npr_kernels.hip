@@ -1008,6 +1008,7 @@ constexpr int kResRing = 2;               // LDS tile slots per wave (1 processe
 constexpr int kDmaPer = kRows + 1;        // DMA instructions per staged tile
 constexpr uint32_t kResWg = 16;           // waves per workgroup (one workgroup per CU): folded in LDS
 static_assert(kResWg >= kResWgMin, "workgroup aggregate slots (npr_capi.hip group_slots) are sized for kResWgMin");
+static_assert(kResWg == kResWgMin, "the host's per-workgroup tile split (ParseParams::wg_q) counts kResWgMin waves");
 static_assert(kResRing >= 2 && (kResRing - 1) * kDmaPer < 64, "vmcnt field is 6 bits");
 
 struct ResShared {  // one wave's LDS
@@ -1017,13 +1018,38 @@ struct ResShared {  // one wave's LDS
 
 // wave v's tiles: q = ntiles / nwaves each, one more for the first ntiles % nwaves waves (the
 // last-dispatched waves start latest, so they get the shorter ranges)
+// Whole workgroups (kp.wg_q != 0): workgroup b holds wg_q tiles, one more for b < wg_r, so every CU
+// parses the same number (C2: 76-77 tiles, where the per-wave split gave 80 or 64); its waves split
+// them in order, the extra tiles going to the lowest waves -- the oldest on each SIMD, which the
+// arbiter favours (per-wave phase A ended 1.7 us later for waves 12-15 than for waves 0-3 of a
+// workgroup, profiles/r06_stamps_rereads.txt).  Otherwise q = ntiles / nwaves per wave.
+__device__ __forceinline__ void res_wg_range(const ParseParams &kp, uint32_t b, uint32_t &g0, uint32_t &gs) {
+  g0 = b * kp.wg_q + (b < kp.wg_r ? b : kp.wg_r);
+  gs = kp.wg_q + (b < kp.wg_r ? 1u : 0u);
+}
 __device__ __forceinline__ void res_range(const ParseParams &kp, uint32_t v, uint32_t &c0, uint32_t &c1) {
+  if (kp.wg_q) {
+    uint32_t g0, gs;
+    res_wg_range(kp, v / kResWg, g0, gs);
+    const uint32_t w = v % kResWg, q = gs / kResWg, r = gs % kResWg;
+    c0 = g0 + w * q + (w < r ? w : r);
+    c1 = c0 + q + (w < r ? 1u : 0u);
+    return;
+  }
   const uint32_t q = kp.ntiles / kp.nwaves, r = kp.ntiles % kp.nwaves;
   c0 = v * q + (v < r ? v : r);
   c1 = c0 + q + (v < r ? 1u : 0u);
 }
 // the wave whose range holds tile m
 __device__ __forceinline__ uint32_t res_wave_of(const ParseParams &kp, int64_t m) {
+  if (kp.wg_q) {
+    const uint32_t t = (uint32_t)m, big = kp.wg_r * (kp.wg_q + 1u);
+    const uint32_t b = t < big ? t / (kp.wg_q + 1u) : kp.wg_r + (t - big) / kp.wg_q;
+    uint32_t g0, gs;
+    res_wg_range(kp, b, g0, gs);
+    const uint32_t q = gs / kResWg, r = gs % kResWg, u = t - g0, big2 = r * (q + 1u);
+    return b * kResWg + (u < big2 ? u / (q + 1u) : r + (u - big2) / q);
+  }
   const uint32_t q = kp.ntiles / kp.nwaves, r = kp.ntiles % kp.nwaves;
   const uint64_t big = (uint64_t)r * (q + 1);
   return (uint64_t)m < big ? (uint32_t)((uint64_t)m / (q + 1)) : (uint32_t)(r + ((uint64_t)m - big) / q);
@@ -1069,11 +1095,8 @@ __device__ __forceinline__ uint64_t ld_res(uint64_t *p) {
   return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // one lane's element of a window: lvl 0 = wave v's A, lvl 1 = workgroup b's aggregate G(b)
-__device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr, bool sc1 = false) {
-  LaneSeg L{};
-  L.mism = -1;
-  L.valid = true;
-  if (!inr) return L;
+// the tiles [first, last] of element idx (lvl 0: wave idx; lvl 1: workgroup idx)
+__device__ __forceinline__ void res_tiles(const ParseParams &kp, int lvl, int64_t idx, LaneSeg &L) {
   uint32_t c0, c1, d0, d1;
   const uint32_t v0 = lvl == 0 ? (uint32_t)idx : (uint32_t)idx * kResWg;
   const uint32_t v1 = lvl == 0 ? (uint32_t)idx : v0 + kResWg - 1u < kp.nwaves - 1 ? v0 + kResWg - 1u : kp.nwaves - 1;
@@ -1081,6 +1104,16 @@ __device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int6
   res_range(kp, v1, d0, d1);
   L.first = c0;
   L.last = (int64_t)d1 - 1;
+}
+// (tiles = false: first / last left for the caller -- the look-back sets them once its windows
+// are in, so they are not live across its polls)
+__device__ __forceinline__ LaneSeg load_res(const ParseParams &kp, int lvl, int64_t idx, bool inr, bool sc1 = false,
+                                            bool tiles = true) {
+  LaneSeg L{};
+  L.mism = -1;
+  L.valid = true;
+  if (!inr) return L;
+  if (tiles) res_tiles(kp, lvl, idx, L);
   const uint32_t ep = kp.epoch;
   uint64_t *w = lvl == 0 ? kp.rslots[idx].a : kp.rgroups[idx].g;
   uint64_t w0, w1, w2, w3, w4;
@@ -1773,7 +1806,7 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
 #pragma unroll
     for (int w = 0; w < kTopWin; ++w) {  // descending inside a window (fold_window's order)
       const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
-      G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true);
+      G[w] = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, (uint32_t)lane < sz, true, false);
     }
     // every window at once: re-read (returning atomics) only the aggregates not yet this
     // launch's -- not published yet, or a line an earlier launch left in this XCD's L2
@@ -1796,10 +1829,15 @@ __device__ __forceinline__ bool res_capture(const ParseParams &kp, ResWgShared &
         const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
         const bool need = (uint32_t)lane < sz && !G[w].present;
         if (__ballot(need)) {
-          const LaneSeg N = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, need);
+          const LaneSeg N = load_res(kp, 1, (int64_t)w0 + sz - 1 - lane, need, false, false);
           if (need) G[w] = N;
         }
       }
+    }
+#pragma unroll
+    for (int w = 0; w < kTopWin; ++w) {  // the windows' tiles
+      const uint32_t w0 = 64u * (uint32_t)w, sz = b > w0 ? (b - w0 < 64u ? b - w0 : 64u) : 0u;
+      if ((uint32_t)lane < sz) res_tiles(kp, 1, (int64_t)w0 + sz - 1 - lane, G[w]);
     }
     if (DIAG) stamp_at(st, 13);
     if (DIAG && kp.stats && lane == 0 && tries) atomicAdd(kp.stats + kStatLbPolls, (uint32_t)tries);
