@@ -89,7 +89,7 @@ def cpu_baseline(blob, n_records, budget_s, sample):
 # The PMC summaries bench.py quotes as roofline.traffic: fixed names, rewritten once per round by
 # scripts/pmc.sh + scripts/pmc_summary.py (never "the newest file": an experiment's summary must not
 # become the bench's traffic by sorting first).
-PMC_SUMMARY = {"c2": "r06_pmc_c2.json", "c3": "r06_pmc_c3.json"}
+PMC_SUMMARY = {"c2": "r06g_pmc_c2.json", "c3": "r06g_pmc_c3.json"}
 
 
 def pmc_traffic(records, config="c2"):
